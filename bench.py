@@ -1,0 +1,255 @@
+"""Benchmark: device-resident GiB/s hashed to a Merkle root (BASELINE.json metric), 1..8 MI355X.
+
+One step = one full Merkle root (leaf SHA-256 + tree reduce) over this rank's share of one
+synthetic object already resident in HBM.  Weak scaling: every rank holds `--object-gib`
+(default 8 GiB = BASELINE configs[1]); at N GPUs the object is N x 8 GiB, sharded by aligned
+chunk ranges, with one RCCL all-gather of subtree roots before rank 0's final levels.
+
+Rank 0 prints ONE JSON line.  At N = 1 it also reports: the K1 roofline (HIP events on the launch
+stream over the timed region), the CPU baseline (the oracle's faithful serial restatement of
+common/hashtree timed on this host over the same bytes), full-size parity (GPU root == CPU root),
+a chunk-size sweep and the host-buffer end-to-end rate.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_LANE_OPS_PEAK = 256 * 128 * 2.4e9   # 256 CU x 4 SIMD-32 x 2.4 GHz (int32 lane-ops/s)
+SEED = 0xDE0550002               # configs[1] seed (0xDE0550000 + k)
+
+
+def env_int(name, default):
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def blocks_for(length: int, chunk: int) -> int:
+    """Compression blocks of the whole tree: sum ceil((len+9)/64) + 2 x nodes."""
+    n = (length + chunk - 1) // chunk
+    last = length - (n - 1) * chunk
+    leaf_blocks = (n - 1) * ((chunk + 9 + 63) // 64) + (last + 9 + 63) // 64
+    nodes, m, levels = 0, n, 0
+    while levels == 0 or m > 1:
+        m = (m + 1) // 2
+        nodes += m
+        levels += 1
+    return leaf_blocks + 2 * nodes
+
+
+def load_traffic(kernel_hint: str):
+    """PMC HBM bytes per K1 launch from the committed rocprofv3 summary, if present."""
+    path = os.path.join(ROOT, "profiles", "k1_traffic.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    return d.get("hbm_bytes_per_launch"), d
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--object-gib", type=float, default=8.0, help="object bytes per GPU (GiB)")
+    ap.add_argument("--chunk", type=int, default=32 << 20, help="chunk (leaf) bytes; default 32 MiB")
+    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from deoss_amd import MerkleContext, plan_shards
+    from deoss_amd.sharding import sharded_root
+
+    world = env_int("WORLD_SIZE", 1)
+    rank = env_int("RANK", 0)
+    local_rank = env_int("LOCAL_RANK", 0)
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+
+    per_gpu = int(args.object_gib * (1 << 30))
+    chunk = args.chunk
+    total = per_gpu * world
+    plan = plan_shards(total, chunk, world)
+    b0, b1 = plan.byte_range(rank)
+    local_len = b1 - b0
+    ctx = MerkleContext(devices=[local_rank])
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    buf = torch.empty(local_len + 64, dtype=torch.uint8, device=device)
+    ctx.fill_synthetic_async(buf.data_ptr(), b0, (local_len + 7) // 8 * 8, SEED, sptr)
+    root_dev = torch.zeros(32, dtype=torch.uint8, device=device)
+    nodes_dev = torch.zeros(max(plan.node_count(rank), 1) * 32, dtype=torch.uint8, device=device)
+
+    def subtree(k):
+        ctx.subtree_device_async(buf.data_ptr(), local_len, chunk, k, nodes_dev.data_ptr(), sptr)
+        return nodes_dev
+
+    def finish(nodes, n, min_one):
+        ctx.finish_device_async(nodes.data_ptr(), n, min_one, root_dev.data_ptr(), sptr)
+        return root_dev
+
+    def step():
+        if world == 1:
+            ctx.root_device_async(buf.data_ptr(), local_len, chunk, root_dev.data_ptr(), 0, sptr)
+        else:
+            sharded_root(plan, rank, subtree, finish, torch, dist, device)
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local_rank])
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.set_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    t1 = time.perf_counter()
+    ncalls, k1_ms_sum, call_ms_sum, k1_ms_max = ctx.timing_summary()
+    ctx.set_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    root_hex = bytes(root_dev.cpu().numpy()).hex() if rank == 0 else None
+
+    value = total * args.steps / elapsed / (1 << 30)
+    k1_avg_ms = k1_ms_sum / max(ncalls, 1)
+    k1_bytes = local_len + 32 * ((local_len + chunk - 1) // chunk)   # read N once + 32 B per leaf
+    achieved_gbs = k1_bytes / (k1_avg_ms * 1e-3) / 1e9 if k1_avg_ms > 0 else 0.0
+    blocks = blocks_for(local_len, chunk)
+    from deoss_amd.isa import valu_per_block
+    vpb = valu_per_block()
+    traffic, traffic_src = load_traffic("leaf_kernel")
+
+    out = {
+        "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling",
+        "value": round(value, 4),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: splitmix64 bytes generated in HBM (same generator as the CPU oracle)",
+        "config": {
+            "workload": f"1 object of {args.object_gib:g} GiB per GPU ({total} B total), chunk {chunk} B "
+                        f"({plan.n_leaves} leaves) - BASELINE configs[1] at N=1, configs[3] shape at N=8",
+            "object_bytes": total, "chunk": chunk, "leaves": plan.n_leaves,
+            "parallelism": f"chunk-range shards (2^{plan.k} leaves per block), 1 process per GPU, "
+                           f"RCCL all-gather of subtree roots" if world > 1 else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm", "kernel": "leaf_kernel (K1)",
+            "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
+            "traffic": traffic, "traffic_source": traffic_src.get("source") if traffic_src else None,
+            "k1_avg_ms": round(k1_avg_ms, 4), "k1_launches": ncalls,
+            "algorithmic_bytes_per_launch": k1_bytes,
+            "valu": {
+                "ops_per_block": vpb, "blocks_per_step": blocks,
+                "achieved_lane_ops_per_s": (blocks * vpb / (k1_avg_ms * 1e-3)) if (vpb and k1_avg_ms) else None,
+                "peak_lane_ops_per_s": VALU_LANE_OPS_PEAK,
+                "frac": (blocks * vpb / (k1_avg_ms * 1e-3) / VALU_LANE_OPS_PEAK) if (vpb and k1_avg_ms) else None,
+                "note": "binding bound for SHA-256 is integer VALU issue, not HBM (DESIGN.md)",
+            },
+        },
+        "root": root_hex,
+    }
+
+    if world == 1 and rank == 0:
+        extras(args, ctx, torch, buf, local_len, chunk, root_hex, out, sptr)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier(device_ids=[local_rank])
+        dist.destroy_process_group()
+
+
+def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    from oracle import Oracle   # CPU baseline / checker only
+    orc = Oracle()
+    host = None
+    if not args.no_cpu or not args.no_e2e:
+        host = torch.empty(length, dtype=torch.uint8, pin_memory=True)
+        host.copy_(buf[:length])
+        torch.cuda.synchronize()
+    if not args.no_cpu:
+        # faithful serial restatement of common/hashtree over the same 8 GiB (1 core, SHA-NI when present)
+        t0 = time.perf_counter()
+        _, cpu_root = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=1)
+        t1 = time.perf_counter()
+        nthr = min(16, os.cpu_count() or 1)
+        _, cpu_root_p = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=nthr)
+        t2 = time.perf_counter()
+        out["cpu_baseline"] = {
+            "value": round(length / (t1 - t0) / (1 << 30), 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"the full {length} B object of the timed workload, chunk {chunk}, serial leaves then tree "
+                      f"(oracle/merkle_oracle.c, SHA-256 backend {orc.backend()}; stands in for Go crypto/sha256)",
+            "parallel": {"value": round(length / (t2 - t1) / (1 << 30), 4), "cores": nthr},
+        }
+        out["parity"] = {"gpu_root": root_hex, "cpu_root": cpu_root.hex(),
+                         "bit_exact": cpu_root.hex() == root_hex and cpu_root_p == cpu_root}
+    if not args.no_e2e and host is not None:
+        # host pinned buffer -> H2D (overlapped) -> root -> 32 B back (the upload-handler path)
+        ctx.root_buffer_ptr(host.data_ptr(), min(length, 64 << 20), chunk)   # warm staging
+        t0 = time.perf_counter()
+        _, r = ctx.root_buffer_ptr(host.data_ptr(), length, chunk)
+        t1 = time.perf_counter()
+        out["e2e"] = {"pinned_host_gibs": round(length / (t1 - t0) / (1 << 30), 4),
+                      "root_matches": r.hex() == root_hex}
+    if not args.no_sweep:
+        sweep = []
+        root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
+        for c in [int(x) for x in args.sweep_chunks.split(",")]:
+            reps = 3 if c < (8 << 20) else 2
+            ctx.root_device_async(buf.data_ptr(), length, c, root.data_ptr(), 0, sptr)
+            torch.cuda.synchronize()
+            ctx.set_timing(True)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.root_device_async(buf.data_ptr(), length, c, root.data_ptr(), 0, sptr)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            n, k1, tot, _ = ctx.timing_summary()
+            ctx.set_timing(False)
+            gpu_root = bytes(root.cpu().numpy())
+            entry = {"chunk": c, "leaves": (length + c - 1) // c,
+                     "gibs": round(length * reps / (t1 - t0) / (1 << 30), 3),
+                     "k1_gbs": round(length / (k1 / n * 1e-3) / 1e9, 2),
+                     "k1_hbm_frac": round(length / (k1 / n * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
+            if host is not None and not args.no_cpu:
+                _, cr = orc.root_buffer_ptr(host.data_ptr(), length, c, nthreads=min(16, os.cpu_count() or 1))
+                entry["bit_exact"] = cr == gpu_root
+            sweep.append(entry)
+        out["sweep"] = sweep
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,91 @@
+"""Loader for ``libdeoss_merkle.so`` (the HIP/gfx950 Merkle path behind include/deoss_merkle.h).
+
+There is no CPU fallback anywhere in this package: if the shared library is missing, or no GPU
+is visible, calls raise :class:`DeossMerkleError`.  The library is built in-tree by
+``__graft_entry__.build()`` (or ``python -m deoss_amd.build``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libdeoss_merkle.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+
+DM_OK = 0
+DM_ERR_EMPTY = -1
+DM_ERR_INVALID = -2
+DM_ERR_HIP = -3
+DM_ERR_RCCL = -4
+DM_ERR_NOMEM = -5
+DM_ERR_IO = -6
+DM_ERR_NODEV = -7
+
+# Every symbol include/deoss_merkle.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = (
+    "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count",
+    "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
+    "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
+    "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_set_timing", "dm_timing_summary",
+)
+
+
+class DeossMerkleError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(message)
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    pvp, pu64 = ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)
+    sigs = {
+        "dm_create": ([ctypes.POINTER(vp), ctypes.POINTER(i32), i32], i32),
+        "dm_destroy": ([vp], None),
+        "dm_strerror": ([i32], ctypes.c_char_p),
+        "dm_last_error": ([vp], ctypes.c_char_p),
+        "dm_device_count": ([vp], i32),
+        "dm_new_hash_tree": ([vp, ctypes.POINTER(ctypes.c_char_p), u64, vp, vp], i32),
+        "dm_root_chunks": ([vp, pvp, pu64, u64, vp, vp], i32),
+        "dm_root_buffer": ([vp, vp, u64, u64, vp, vp], i32),
+        "dm_root_batch": ([vp, pvp, pu64, u64, u64, vp], i32),
+        "dm_root_device": ([vp, vp, u64, u64, vp], i32),
+        "dm_root_device_async": ([vp, vp, u64, u64, vp, vp, vp], i32),
+        "dm_subtree_device_async": ([vp, vp, u64, u64, u32, vp, pu64, vp], i32),
+        "dm_finish_device_async": ([vp, vp, u64, i32, vp, vp], i32),
+        "dm_root_batch_device_async": ([vp, pvp, pu64, u64, u64, vp, vp], i32),
+        "dm_fill_synthetic_async": ([vp, vp, u64, u64, u64, vp], i32),
+        "dm_set_timing": ([vp, i32], i32),
+        "dm_timing_summary": ([vp, pu64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                               ctypes.POINTER(ctypes.c_double)], i32),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the HIP library; raises (never falls back) when it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise DeossMerkleError(
+                DM_ERR_NODEV,
+                f"{path} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        L = ctypes.CDLL(path)
+        _declare(L)
+        _lib = L
+        return L
+
+
+def strerror(code: int) -> str:
+    return load_library().dm_strerror(code).decode()

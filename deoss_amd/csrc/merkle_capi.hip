@@ -1,0 +1,934 @@
+// merkle_capi.hip -- host runtime and C ABI (include/deoss_merkle.h) of the MI355X Merkle path.
+//
+// Replaces, behind a C ABI, DeOSS common/hashtree (common/hashtree/types.go:19-39,
+// common/hashtree/hashtree.go:18-35) and the tree construction of cbergoon/merkletree v0.2.0
+// (go.mod:10).  Every entry point returns an error code; there is no CPU fallback: a missing
+// or failing GPU is reported as DM_ERR_NODEV / DM_ERR_HIP.
+//
+// Layout of one call (single device):
+//   object bytes in HBM --K1 leaf_kernel (SHA-256 per chunk, first <=8 levels fused in LDS)-->
+//   level-L nodes --K2 reduce_kernel (<=9 levels per launch)--> ... --> 32-byte root.
+// Multi-device (one process, ndev > 1): aligned chunk ranges per device, per-device subtree
+// roots, one RCCL all-gather of the 32-byte roots, final levels on the first device.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "deoss_merkle.h"
+#include "merkle_kernels.hpp"
+
+namespace {
+
+constexpr uint64_t kAlign = 256;                    // leaf start alignment when packing chunks
+constexpr uint64_t kStageBytes = 64ull << 20;       // pinned staging slot
+constexpr uint64_t kStripeBudget = 256ull << 20;    // bytes per H2D stripe / batch (e2e path)
+
+uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
+uint32_t ceil_log2(uint64_t n) {
+    uint32_t d = 0;
+    while ((1ull << d) < n) d++;
+    return d;
+}
+uint64_t ceil_shift(uint64_t n, uint32_t k) { return k >= 64 ? (n ? 1 : 0) : (n + (1ull << k) - 1) >> k; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipDeviceSynchronize();   // scratch may still be in use by queued work
+            if (e != hipSuccess) return e;
+            (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+        }
+        size_t c = round_up(std::max<size_t>(n, 4096), 2ull << 20);
+        hipError_t e = hipMalloc(&p, c);
+        if (e != hipSuccess) return e;
+        cap = c;
+        return hipSuccess;
+    }
+    uint8_t* u8() { return static_cast<uint8_t*>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        cap = n;
+        return hipSuccess;
+    }
+    uint8_t* u8() { return static_cast<uint8_t*>(p); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Dev {
+    int id = 0;
+    hipStream_t stream = nullptr;       // compute stream
+    hipStream_t copy = nullptr;         // H2D stream
+    DevBuf data, nodes_a, nodes_b, leaves, tab_addr, tab_len, tab_first, tab_ids, root, gather;
+    PinnedBuf stage[2];
+    PinnedBuf htab;                     // pinned bounce buffer for per-call index tables
+    uint64_t htab_used = 0;
+    hipEvent_t ev_done = nullptr;
+    hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_htab = nullptr;
+    hipStream_t last_stream = nullptr;  // stream of the last enqueued call (scratch ordering)
+    // timing records: (K1 begin, K1 end, call end) per timed call, reused across resets
+    std::vector<hipEvent_t> tev;
+    size_t ntimed = 0;
+};
+
+}  // namespace
+
+struct dm_ctx {
+    std::mutex mu;
+    std::vector<Dev> devs;
+    std::vector<ncclComm_t> comms;
+    std::string err;
+    bool timing = false;
+};
+
+namespace {
+
+int fail(dm_ctx* c, int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(c, e_ == hipErrorOutOfMemory ? DM_ERR_NOMEM : DM_ERR_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(e_), __FILE__, __LINE__);                    \
+    } while (0)
+
+#define RC_TRY(expr)                 \
+    do {                             \
+        int rc_ = (expr);            \
+        if (rc_ != DM_OK) return rc_; \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                         \
+    do {                                                                                       \
+        ncclResult_t r_ = (expr);                                                              \
+        if (r_ != ncclSuccess)                                                                 \
+            return fail(c, DM_ERR_RCCL, "%s: %s", #expr, ncclGetErrorString(r_));              \
+    } while (0)
+
+hipStream_t pick_stream(Dev& d, void* s) { return s ? static_cast<hipStream_t>(s) : d.stream; }
+
+// Order this call's use of the context scratch after the previous call's (possibly other stream).
+int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
+    HIP_TRY(hipSetDevice(d.id));
+    if (d.last_stream != nullptr && d.last_stream != s) {
+        HIP_TRY(hipEventRecord(d.ev_done, d.last_stream));
+        HIP_TRY(hipStreamWaitEvent(s, d.ev_done, 0));
+    }
+    d.last_stream = s;
+    return DM_OK;
+}
+
+bool is_aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Next timing record (3 events) of device d; nullptr when timing is off.
+hipEvent_t* timing_record(dm_ctx* c, Dev& d) {
+    if (!c->timing) return nullptr;
+    const size_t need = 3 * (d.ntimed + 1);
+    while (d.tev.size() < need) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        d.tev.push_back(e);
+    }
+    return &d.tev[3 * d.ntimed++];
+}
+
+// Start a call's table uploads: wait until the previous call's uploads have left the bounce buffer.
+int tables_begin(dm_ctx* c, Dev& d, uint64_t bytes) {
+    HIP_TRY(hipEventSynchronize(d.ev_htab));
+    HIP_TRY(d.htab.ensure(std::max<uint64_t>(round_up(bytes, 256) + 4096, 1ull << 20)));
+    d.htab_used = 0;
+    return DM_OK;
+}
+
+// Stream-ordered upload of a host table through the pinned bounce buffer (host memory may be
+// released as soon as this returns).
+int upload(dm_ctx* c, Dev& d, hipStream_t s, DevBuf& dst, const void* src, uint64_t bytes) {
+    HIP_TRY(dst.ensure(std::max<uint64_t>(bytes, 8)));
+    if (bytes == 0) return DM_OK;
+    if (d.htab_used + bytes > d.htab.cap) return fail(c, DM_ERR_INVALID, "table bounce buffer overflow");
+    uint8_t* h = d.htab.u8() + d.htab_used;
+    std::memcpy(h, src, bytes);
+    d.htab_used = round_up(d.htab_used + bytes, 256);
+    HIP_TRY(hipMemcpyAsync(dst.p, h, bytes, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(d.ev_htab, s));
+    return DM_OK;
+}
+
+// K2 stages: reduce m nodes at `in` for exactly D levels (D >= 1) into dst.
+int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t m, uint32_t D, uint8_t* dst) {
+    std::vector<uint32_t> ks;
+    for (uint32_t r = D; r > 0;) {
+        uint32_t k = std::min<uint32_t>(9, r);
+        ks.push_back(k);
+        r -= k;
+    }
+    HIP_TRY(d.nodes_a.ensure(std::max<uint64_t>(ceil_div(m, 2), 1) * 32));
+    HIP_TRY(d.nodes_b.ensure(std::max<uint64_t>(ceil_div(m, 2), 1) * 32));
+    const uint8_t* cur = in;
+    for (size_t i = 0; i < ks.size(); i++) {
+        uint8_t* out = (i + 1 == ks.size()) ? dst : (cur == d.nodes_a.u8() ? d.nodes_b.u8() : d.nodes_a.u8());
+        const uint64_t grid = ceil_div(m, dm::kReduceTile);
+        hipLaunchKernelGGL(dm::reduce_kernel, dim3((uint32_t)grid), dim3(dm::kBlock), 0, s, cur, m, ks[i], out);
+        HIP_TRY(hipGetLastError());
+        m = ceil_shift(m, ks[i]);
+        cur = out;
+    }
+    return DM_OK;
+}
+
+// Hash the leaves described by `la` (uniform or table mode) and reduce `levels` levels
+// (levels < 0: to the root, >= 1 level).  Nodes go to dst; *nout gets their count.
+int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool aligned, int levels,
+             uint8_t* dst, uint64_t* nout, uint8_t* leaf_dig) {
+    const uint64_t n = la.nleaves;
+    const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
+    const uint32_t L1 = std::min<uint32_t>(dm::kLeafFuseMax, D);
+    const uint64_t m1 = ceil_shift(n, L1);
+    la.byte_off = 0;
+    la.byte_end = ~0ull;
+    la.state = nullptr;
+    la.fuse_levels = L1;
+    uint8_t* k1_out = dst;
+    if (D > L1) {
+        HIP_TRY(d.leaves.ensure(m1 * 32));   // level-L1 nodes
+        k1_out = d.leaves.u8();
+    }
+    if (L1 == 0) {
+        la.digests = dst;
+        la.level_out = nullptr;
+    } else {
+        la.digests = leaf_dig;
+        la.level_out = k1_out;
+    }
+    hipEvent_t* tr = timing_record(c, d);
+    if (tr) HIP_TRY(hipEventRecord(tr[0], s));
+    const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
+    if (table) {
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+    } else {
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+    }
+    HIP_TRY(hipGetLastError());
+    if (tr) HIP_TRY(hipEventRecord(tr[1], s));
+    if (L1 == 0 && leaf_dig != nullptr && leaf_dig != dst)
+        HIP_TRY(hipMemcpyAsync(leaf_dig, dst, n * 32, hipMemcpyDeviceToDevice, s));
+    if (D > L1) RC_TRY(reduce_stages(c, d, s, k1_out, m1, D - L1, dst));
+    if (tr) HIP_TRY(hipEventRecord(tr[2], s));
+    *nout = ceil_shift(n, D);
+    return DM_OK;
+}
+
+dm::LeafArgs uniform_args(const void* dev, uint64_t len, uint64_t chunk) {
+    dm::LeafArgs la{};
+    const uint64_t n = ceil_div(len, chunk);
+    la.base = static_cast<const uint8_t*>(dev);
+    la.pitch = chunk;
+    la.leaf_len = chunk;
+    la.last_len = len - (n - 1) * chunk;
+    la.nleaves = n;
+    return la;
+}
+
+// Finish: reduce n nodes to the root (>= 1 level if min_one or n > 1).
+int finish(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* nodes, uint64_t n, bool min_one, uint8_t* dst) {
+    uint32_t D = ceil_log2(n);
+    if (D == 0 && min_one) D = 1;
+    if (D == 0) {
+        HIP_TRY(hipMemcpyAsync(dst, nodes, 32, hipMemcpyDeviceToDevice, s));
+        return DM_OK;
+    }
+    return reduce_stages(c, d, s, nodes, n, D, dst);
+}
+
+// Batched per-object trees over leaf digests already in d.leaves-like storage.
+int batch_roots_from_leaves(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* leaves,
+                            const std::vector<uint64_t>& first, uint8_t* roots) {
+    const uint64_t nobj = first.size() - 1;
+    std::vector<uint32_t> small;
+    small.reserve(nobj);
+    for (uint64_t o = 0; o < nobj; o++)
+        if (first[o + 1] - first[o] <= (uint64_t)dm::kReduceTile) small.push_back((uint32_t)o);
+    if (!small.empty()) {
+        RC_TRY(upload(c, d, s, d.tab_first, first.data(), first.size() * 8));
+        RC_TRY(upload(c, d, s, d.tab_ids, small.data(), small.size() * 4));
+        hipLaunchKernelGGL(dm::batch_root_kernel, dim3((uint32_t)small.size()), dim3(dm::kBlock), 0, s,
+                           leaves, static_cast<const uint64_t*>(d.tab_first.p),
+                           static_cast<const uint32_t*>(d.tab_ids.p), roots);
+        HIP_TRY(hipGetLastError());
+    }
+    for (uint64_t o = 0; o < nobj; o++) {
+        const uint64_t cnt = first[o + 1] - first[o];
+        if (cnt <= (uint64_t)dm::kReduceTile) continue;
+        RC_TRY(finish(c, d, s, leaves + 32 * first[o], cnt, true, roots + 32 * o));
+    }
+    return DM_OK;
+}
+
+// Leaf hashing of a batch of objects at device addresses + per-object roots.
+int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, const uint64_t* lens, uint64_t nobj,
+                 uint64_t chunk, uint8_t* roots) {
+    std::vector<uint64_t> first(nobj + 1, 0);
+    for (uint64_t o = 0; o < nobj; o++) {
+        if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
+        first[o + 1] = first[o] + ceil_div(lens[o], chunk);
+    }
+    const uint64_t T = first[nobj];
+    std::vector<uint64_t> addr(T), len(T);
+    bool aligned = true;
+    for (uint64_t o = 0; o < nobj; o++) {
+        const uint64_t n = first[o + 1] - first[o];
+        for (uint64_t j = 0; j < n; j++) {
+            const uint64_t a = reinterpret_cast<uint64_t>(objs[o]) + j * chunk;
+            addr[first[o] + j] = a;
+            len[first[o] + j] = (j + 1 < n) ? chunk : lens[o] - j * chunk;
+            aligned &= (a & 15) == 0;
+        }
+    }
+    RC_TRY(tables_begin(c, d, T * 16 + (nobj + 1) * 12 + 1024));
+    HIP_TRY(d.leaves.ensure(T * 32));
+    RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), T * 8));
+    RC_TRY(upload(c, d, s, d.tab_len, len.data(), T * 8));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(d.tab_addr.p);
+    la.lens = static_cast<const uint64_t*>(d.tab_len.p);
+    la.nleaves = T;
+    la.byte_end = ~0ull;
+    la.digests = d.leaves.u8();
+    hipEvent_t* tr = timing_record(c, d);
+    if (tr) HIP_TRY(hipEventRecord(tr[0], s));
+    const uint32_t grid = (uint32_t)ceil_div(T, dm::kBlock);
+    if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+    else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+    HIP_TRY(hipGetLastError());
+    if (tr) HIP_TRY(hipEventRecord(tr[1], s));
+    RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, roots));
+    if (tr) HIP_TRY(hipEventRecord(tr[2], s));
+    return DM_OK;
+}
+
+// Pack host chunks into device memory (256-B aligned starts) through the pinned ring.
+// Returns the device address of each chunk in `addr`.
+int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uint64_t n,
+                std::vector<uint64_t>& addr) {
+    std::vector<uint64_t> off(n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        off[i] = total;
+        total = round_up(total + lens[i], kAlign);
+    }
+    HIP_TRY(d.data.ensure(std::max<uint64_t>(total, kAlign)));
+    addr.resize(n);
+    for (uint64_t i = 0; i < n; i++) addr[i] = reinterpret_cast<uint64_t>(d.data.u8() + off[i]);
+    HIP_TRY(d.stage[0].ensure(kStageBytes));
+    HIP_TRY(d.stage[1].ensure(kStageBytes));
+    int slot = 0;
+    bool busy[2] = {false, false};
+    uint64_t fill = 0, slot_dev_off = 0;
+    auto flush = [&]() -> int {
+        if (fill == 0) return DM_OK;
+        HIP_TRY(hipMemcpyAsync(d.data.u8() + slot_dev_off, d.stage[slot].p, fill, hipMemcpyHostToDevice, d.copy));
+        HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
+        busy[slot] = true;
+        slot ^= 1;
+        if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
+        busy[slot] = false;
+        fill = 0;
+        return DM_OK;
+    };
+    for (uint64_t i = 0; i < n; i++) {
+        const uint64_t span = round_up(lens[i], kAlign);
+        if (lens[i] > kStageBytes) {   // large chunk: direct copy (pageable source, synchronous)
+            RC_TRY(flush());
+            HIP_TRY(hipMemcpyAsync(d.data.u8() + off[i], ptrs[i], lens[i], hipMemcpyHostToDevice, d.copy));
+            continue;
+        }
+        if (fill != 0 && (off[i] != slot_dev_off + fill || fill + span > kStageBytes)) RC_TRY(flush());
+        if (fill == 0) slot_dev_off = off[i];
+        if (lens[i]) std::memcpy(d.stage[slot].u8() + fill, ptrs[i], lens[i]);
+        fill += span;
+    }
+    RC_TRY(flush());
+    HIP_TRY(hipStreamSynchronize(d.copy));
+    return DM_OK;
+}
+
+// Host object buffer -> HBM, hashing overlapped with the H2D copies.  Leaf digests land in
+// d.leaves; the caller reduces them.  Stripes: every leaf advances by W bytes per step, so all
+// leaves stay in flight (large-chunk case); when W covers a whole chunk this is one step of
+// contiguous copies.
+int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint64_t chunk) {
+    const uint64_t n = ceil_div(len, chunk);
+    const uint64_t last_len = len - (n - 1) * chunk;
+    HIP_TRY(d.data.ensure(len));
+    HIP_TRY(d.leaves.ensure(n * 32));
+    hipPointerAttribute_t attr{};
+    bool pinned = false;
+    if (hipPointerGetAttributes(&attr, host) == hipSuccess)
+        pinned = attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();   // clear the error of an unregistered pointer
+    const bool aligned = (chunk % 16) == 0;
+    // Many leaves: hashing runs at >= 100x the PCIe rate, so copy then hash in one launch.
+    // Few large leaves (latency-bound hashing): stripes keep every leaf in flight while copying.
+    const bool contiguous = n >= 4096 || len <= kStripeBudget;
+    dm::LeafArgs la{};
+    la.pitch = chunk;
+    la.leaf_len = chunk;
+    la.last_len = last_len;
+    la.digests = d.leaves.u8();
+    hipStream_t s = d.stream;
+    if (contiguous) {
+        // one hashing step over all leaves; copies in <= kStageBytes pieces
+        HIP_TRY(d.stage[0].ensure(kStageBytes));
+        HIP_TRY(d.stage[1].ensure(kStageBytes));
+        int slot = 0;
+        bool busy[2] = {false, false};
+        for (uint64_t o = 0; o < len; o += kStageBytes) {
+            const uint64_t sz = std::min(kStageBytes, len - o);
+            if (pinned) {
+                HIP_TRY(hipMemcpyAsync(d.data.u8() + o, static_cast<const uint8_t*>(host) + o, sz,
+                                       hipMemcpyHostToDevice, d.copy));
+            } else {
+                if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
+                std::memcpy(d.stage[slot].p, static_cast<const uint8_t*>(host) + o, sz);
+                HIP_TRY(hipMemcpyAsync(d.data.u8() + o, d.stage[slot].p, sz, hipMemcpyHostToDevice, d.copy));
+                HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
+                busy[slot] = true;
+                slot ^= 1;
+            }
+        }
+        HIP_TRY(hipEventRecord(d.ev_copy[0], d.copy));
+        HIP_TRY(hipStreamWaitEvent(s, d.ev_copy[0], 0));
+        la.base = d.data.u8();
+        la.nleaves = n;
+        la.byte_end = ~0ull;
+        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        HIP_TRY(hipGetLastError());
+        return DM_OK;
+    }
+    // striped: W bytes of every leaf per step (W multiple of 64), state carried in HBM
+    const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
+    const uint64_t nsteps = ceil_div(chunk, W);
+    HIP_TRY(d.nodes_b.ensure(n * 32));   // per-leaf chaining state (8 words)
+    uint32_t* state = static_cast<uint32_t*>(d.nodes_b.p);
+    HIP_TRY(d.stage[0].ensure(std::min<uint64_t>(W * n, kStripeBudget)));
+    HIP_TRY(d.stage[1].ensure(std::min<uint64_t>(W * n, kStripeBudget)));
+    bool busy[2] = {false, false};
+    int slot = 0;
+    hipEvent_t* ev_hashed = d.ev_step;
+    for (uint64_t step = 0; step < nsteps; step++) {
+        const uint64_t b0 = step * W;
+        const uint64_t w = std::min(W, chunk - b0);
+        const uint8_t* src = static_cast<const uint8_t*>(host);
+        // rows 0..n-2 are full chunks; row n-1 holds last_len bytes
+        const uint64_t last_w = last_len > b0 ? std::min(w, last_len - b0) : 0;
+        if (pinned) {
+            if (n > 1)
+                HIP_TRY(hipMemcpy2DAsync(d.data.u8() + b0, chunk, src + b0, chunk, w, n - 1, hipMemcpyHostToDevice, d.copy));
+            if (last_w)
+                HIP_TRY(hipMemcpyAsync(d.data.u8() + (n - 1) * chunk + b0, src + (n - 1) * chunk + b0, last_w,
+                                       hipMemcpyHostToDevice, d.copy));
+        } else {
+            if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
+            uint8_t* st = d.stage[slot].u8();
+            for (uint64_t r = 0; r + 1 < n; r++) std::memcpy(st + r * w, src + r * chunk + b0, w);
+            if (last_w) std::memcpy(st + (n - 1) * w, src + (n - 1) * chunk + b0, last_w);
+            if (n > 1)
+                HIP_TRY(hipMemcpy2DAsync(d.data.u8() + b0, chunk, st, w, w, n - 1, hipMemcpyHostToDevice, d.copy));
+            if (last_w)
+                HIP_TRY(hipMemcpyAsync(d.data.u8() + (n - 1) * chunk + b0, st + (n - 1) * w, last_w,
+                                       hipMemcpyHostToDevice, d.copy));
+            HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
+            busy[slot] = true;
+            slot ^= 1;
+        }
+        HIP_TRY(hipEventRecord(ev_hashed[step & 1], d.copy));
+        HIP_TRY(hipStreamWaitEvent(s, ev_hashed[step & 1], 0));
+        la.base = d.data.u8() + b0;
+        la.nleaves = n;
+        la.byte_off = b0;
+        la.byte_end = b0 + w;
+        la.state = state;
+        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        HIP_TRY(hipGetLastError());
+    }
+    return DM_OK;
+}
+
+// Device-resident single object on device d (caller holds the context lock).
+int root_device_impl(dm_ctx* c, Dev& d, hipStream_t s, const void* dev, uint64_t len, uint64_t chunk,
+                     uint8_t* dev_root, uint8_t* leaf_out_dev) {
+    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    RC_TRY(begin_call(c, d, s));
+    dm::LeafArgs la = uniform_args(dev, len, chunk);
+    uint64_t nout = 0;
+    const bool aligned = is_aligned16(dev) && chunk % 16 == 0;
+    return run_tree(c, d, s, la, false, aligned, -1, dev_root, &nout, leaf_out_dev);
+}
+
+int init_device(dm_ctx* c, Dev& d) {
+    HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_copy[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_copy[1], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_step[0], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_step[1], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_htab, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(d.ev_htab, d.stream));
+    HIP_TRY(d.root.ensure(4096));
+    return DM_OK;
+}
+
+void destroy_device(Dev& d) {
+    if (hipSetDevice(d.id) != hipSuccess) return;
+    (void)hipDeviceSynchronize();
+    for (DevBuf* b : {&d.data, &d.nodes_a, &d.nodes_b, &d.leaves, &d.tab_addr, &d.tab_len, &d.tab_first, &d.tab_ids,
+                      &d.root, &d.gather})
+        b->release();
+    d.stage[0].release();
+    d.stage[1].release();
+    d.htab.release();
+    for (hipEvent_t e : {d.ev_done, d.ev_copy[0], d.ev_copy[1], d.ev_step[0], d.ev_step[1], d.ev_htab})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : d.tev) (void)hipEventDestroy(e);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+    if (d.copy) (void)hipStreamDestroy(d.copy);
+}
+
+// D2H of the leaf digests + root of a single-device tree whose leaf digests sit in d.leaves.
+int reduce_leaves_to_host(dm_ctx* c, Dev& d, uint64_t n, uint8_t* leaf_out, uint8_t root[32]) {
+    hipStream_t s = d.stream;
+    uint8_t* droot = d.root.u8();
+    RC_TRY(finish(c, d, s, d.leaves.u8(), n, true, droot));
+    HIP_TRY(hipMemcpyAsync(root, droot, 32, hipMemcpyDeviceToHost, s));
+    if (leaf_out) HIP_TRY(hipMemcpyAsync(leaf_out, d.leaves.p, n * 32, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return DM_OK;
+}
+
+// Multi-device single object from host memory: aligned leaf ranges per device, subtree roots,
+// RCCL all-gather, final levels on device 0.
+int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out,
+                      uint8_t root[32]) {
+    const int G = (int)c->devs.size();
+    const uint64_t n = ceil_div(len, chunk);
+    // block = 2^k leaves with at least 2 blocks per device when possible
+    uint32_t k = 0;
+    while (ceil_shift(n, k + 1) >= (uint64_t)(2 * G)) k++;
+    const uint64_t S = 1ull << k, nb = ceil_shift(n, k);
+    std::vector<uint64_t> b_lo(G), b_hi(G), cnt(G);
+    uint64_t maxc = 0;
+    for (int g = 0; g < G; g++) {
+        b_lo[g] = nb * g / G;
+        b_hi[g] = nb * (g + 1) / G;
+        cnt[g] = b_hi[g] - b_lo[g];
+        maxc = std::max(maxc, cnt[g]);
+    }
+    std::vector<int> rcs(G, DM_OK);
+    std::vector<std::string> errs(G);
+    // per-device: H2D of its byte range + subtree to k levels (parallel host threads)
+    auto work = [&](int g) {
+        Dev& d = c->devs[g];
+        dm_ctx local;   // private error sink
+        dm_ctx* cc = &local;
+        int rc = DM_OK;
+        do {
+            if (hipSetDevice(d.id) != hipSuccess) { rc = DM_ERR_HIP; break; }
+            const uint64_t l0 = b_lo[g] * S, l1 = std::min(n, b_hi[g] * S);
+            if (l1 <= l0) break;
+            const uint64_t byte0 = l0 * chunk, byte1 = std::min(len, l1 * chunk);
+            if (d.data.ensure(byte1 - byte0) != hipSuccess || d.gather.ensure(std::max<uint64_t>(maxc, 1) * 32 * (G + 1)) != hipSuccess) {
+                rc = DM_ERR_NOMEM;
+                break;
+            }
+            if (hipMemcpy(d.data.p, static_cast<const uint8_t*>(host) + byte0, byte1 - byte0, hipMemcpyHostToDevice) != hipSuccess) {
+                rc = DM_ERR_HIP;
+                break;
+            }
+            dm::LeafArgs la = uniform_args(d.data.p, byte1 - byte0, chunk);
+            uint64_t nout = 0;
+            if (leaf_out) {
+                if (d.leaves.ensure((l1 - l0) * 32 + 256) != hipSuccess) { rc = DM_ERR_NOMEM; break; }
+            }
+            // leaf digests for leaf_out are produced by a separate K1 pass only when requested
+            rc = run_tree(cc, d, d.stream, la, false, (chunk % 16) == 0, (int)k, d.gather.u8(), &nout,
+                          nullptr);
+            if (rc != DM_OK) break;
+            if (leaf_out) {
+                dm::LeafArgs lb = uniform_args(d.data.p, byte1 - byte0, chunk);
+                uint64_t n2 = 0;
+                rc = run_tree(cc, d, d.stream, lb, false, (chunk % 16) == 0, 0, d.leaves.u8(), &n2, nullptr);
+                if (rc != DM_OK) break;
+                if (hipMemcpyAsync(leaf_out + 32 * l0, d.leaves.p, (l1 - l0) * 32, hipMemcpyDeviceToHost, d.stream) != hipSuccess) {
+                    rc = DM_ERR_HIP;
+                    break;
+                }
+            }
+        } while (0);
+        rcs[g] = rc;
+        errs[g] = local.err;
+    };
+    {
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; g++) th.emplace_back(work, g);
+        for (auto& t : th) t.join();
+    }
+    for (int g = 0; g < G; g++)
+        if (rcs[g] != DM_OK) return fail(c, rcs[g], "device %d: %s", c->devs[g].id, errs[g].c_str());
+    // C1: all-gather of fixed-size slots (maxc nodes of 32 B per device) over RCCL
+    const size_t slot = maxc * 32;
+    NCCL_TRY(ncclGroupStart());
+    for (int g = 0; g < G; g++) {
+        Dev& d = c->devs[g];
+        NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, c->comms[g], d.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+    Dev& d0 = c->devs[0];
+    HIP_TRY(hipSetDevice(d0.id));
+    // compact the gathered slots into block order on device 0
+    uint64_t total = 0;
+    HIP_TRY(d0.nodes_b.ensure(nb * 32 + 256));
+    for (int g = 0; g < G; g++) {
+        if (cnt[g] == 0) continue;
+        HIP_TRY(hipMemcpyAsync(d0.nodes_b.u8() + 32 * total, d0.gather.u8() + slot + g * slot, cnt[g] * 32,
+                               hipMemcpyDeviceToDevice, d0.stream));
+        total += cnt[g];
+    }
+    // nodes_b is also K2 scratch: move the block roots to `leaves` first
+    HIP_TRY(d0.leaves.ensure(std::max<uint64_t>(nb * 32, n * 32) + 256));
+    HIP_TRY(hipMemcpyAsync(d0.leaves.p, d0.nodes_b.p, nb * 32, hipMemcpyDeviceToDevice, d0.stream));
+    RC_TRY(finish(c, d0, d0.stream, d0.leaves.u8(), nb, k == 0, d0.root.u8()));
+    HIP_TRY(hipMemcpyAsync(root, d0.root.p, 32, hipMemcpyDeviceToHost, d0.stream));
+    for (int g = 0; g < G; g++) {
+        HIP_TRY(hipSetDevice(c->devs[g].id));
+        HIP_TRY(hipStreamSynchronize(c->devs[g].stream));
+    }
+    return DM_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+const char* dm_strerror(int rc) {
+    switch (rc) {
+        case DM_OK: return "ok";
+        case DM_ERR_EMPTY: return "Empty data";
+        case DM_ERR_INVALID: return "invalid argument";
+        case DM_ERR_HIP: return "HIP runtime error";
+        case DM_ERR_RCCL: return "RCCL error";
+        case DM_ERR_NOMEM: return "out of memory";
+        case DM_ERR_IO: return "I/O error";
+        case DM_ERR_NODEV: return "no usable GPU";
+        default: return "unknown error";
+    }
+}
+
+const char* dm_last_error(dm_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+int dm_device_count(dm_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+
+int dm_create(dm_ctx** out, const int* devs, int ndev) {
+    if (!out) return DM_ERR_INVALID;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return DM_ERR_NODEV;
+    std::vector<int> ids;
+    if (!devs || ndev <= 0) ids.push_back(0);
+    else ids.assign(devs, devs + ndev);
+    for (size_t i = 0; i < ids.size(); i++) {
+        if (ids[i] < 0 || ids[i] >= count) return DM_ERR_INVALID;
+        for (size_t j = 0; j < i; j++)
+            if (ids[j] == ids[i]) return DM_ERR_INVALID;
+    }
+    dm_ctx* c = new dm_ctx();
+    c->devs.resize(ids.size());
+    for (size_t i = 0; i < ids.size(); i++) {
+        c->devs[i].id = ids[i];
+        int rc = init_device(c, c->devs[i]);
+        if (rc != DM_OK) {
+            dm_destroy(c);
+            return rc;
+        }
+    }
+    if (ids.size() > 1) {
+        c->comms.resize(ids.size());
+        if (ncclCommInitAll(c->comms.data(), (int)ids.size(), ids.data()) != ncclSuccess) {
+            c->comms.clear();
+            dm_destroy(c);
+            return DM_ERR_RCCL;
+        }
+    }
+    *out = c;
+    return DM_OK;
+}
+
+void dm_destroy(dm_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& cm : ctx->comms) (void)ncclCommDestroy(cm);
+    for (auto& d : ctx->devs) destroy_device(d);
+    delete ctx;
+}
+
+int dm_set_timing(dm_ctx* ctx, int enable) {
+    if (!ctx) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->timing = enable != 0;
+    for (auto& d : ctx->devs) d.ntimed = 0;
+    return DM_OK;
+}
+
+int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double* total_ms_sum, double* leaf_ms_max) {
+    if (!ctx) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    uint64_t n = 0;
+    double a = 0, b = 0, mx = 0;
+    for (auto& d : ctx->devs) {
+        if (d.ntimed == 0) continue;
+        HIP_TRY(hipSetDevice(d.id));
+        HIP_TRY(hipEventSynchronize(d.tev[3 * d.ntimed - 1]));
+        for (size_t i = 0; i < d.ntimed; i++) {
+            float x = 0, y = 0;
+            HIP_TRY(hipEventElapsedTime(&x, d.tev[3 * i], d.tev[3 * i + 1]));
+            HIP_TRY(hipEventElapsedTime(&y, d.tev[3 * i], d.tev[3 * i + 2]));
+            a += x;
+            b += y;
+            mx = std::max(mx, (double)x);
+            n++;
+        }
+    }
+    if (ncalls) *ncalls = n;
+    if (leaf_ms_sum) *leaf_ms_sum = a;
+    if (total_ms_sum) *total_ms_sum = b;
+    if (leaf_ms_max) *leaf_ms_max = mx;
+    return DM_OK;
+}
+
+int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, void* dev_root,
+                         void* leaf_out_dev, void* stream) {
+    if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    Dev& d = ctx->devs[0];
+    return root_device_impl(ctx, d, pick_stream(d, stream), dev, len, chunk, static_cast<uint8_t*>(dev_root),
+                            static_cast<uint8_t*>(leaf_out_dev));
+}
+
+int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint8_t root[32]) {
+    if (!ctx || !root || chunk == 0 || (!dev && len)) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    Dev& d = c->devs[0];
+    RC_TRY(root_device_impl(c, d, d.stream, dev, len, chunk, d.root.u8(), nullptr));
+    HIP_TRY(hipMemcpyAsync(root, d.root.p, 32, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return DM_OK;
+}
+
+int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint32_t levels,
+                            void* dev_nodes, uint64_t* n_out, void* stream) {
+    if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    dm::LeafArgs la = uniform_args(dev, len, chunk);
+    uint64_t nout = 0;
+    const bool aligned = is_aligned16(dev) && chunk % 16 == 0;
+    RC_TRY(run_tree(c, d, s, la, false, aligned, (int)levels, static_cast<uint8_t*>(dev_nodes), &nout, nullptr));
+    if (n_out) *n_out = nout;
+    return DM_OK;
+}
+
+int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int min_one_level, void* dev_root,
+                           void* stream) {
+    if (!ctx || !dev_nodes || !dev_root) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    return finish(c, d, s, static_cast<const uint8_t*>(dev_nodes), n, min_one_level != 0,
+                  static_cast<uint8_t*>(dev_root));
+}
+
+int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const uint64_t* lens, uint64_t nobj,
+                               uint64_t chunk, void* dev_roots, void* stream) {
+    if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (nobj == 0) return DM_OK;
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    return batch_device(c, d, s, dev_objs, lens, nobj, chunk, static_cast<uint8_t*>(dev_roots));
+}
+
+int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbytes, uint64_t seed, void* stream) {
+    if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (nbytes == 0) return DM_OK;
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    const uint64_t nwords = nbytes / 8;
+    const uint64_t grid = std::min<uint64_t>(ceil_div(nwords, 2 * dm::kBlock), 8192);
+    hipLaunchKernelGGL(dm::fill_splitmix_kernel, dim3((uint32_t)grid), dim3(dm::kBlock), 0, s,
+                       static_cast<uint64_t*>(dev), off / 8, nwords, seed);
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
+int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32]) {
+    if (!ctx || !root || chunk == 0 || (!host && len)) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    if (c->devs.size() > 1 && ceil_div(len, chunk) >= 2 * c->devs.size())
+        return root_buffer_multi(c, host, len, chunk, leaf_out, root);
+    Dev& d = c->devs[0];
+    RC_TRY(begin_call(c, d, d.stream));
+    RC_TRY(h2d_and_hash_leaves(c, d, host, len, chunk));
+    return reduce_leaves_to_host(c, d, ceil_div(len, chunk), leaf_out, root);
+}
+
+int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out,
+                   uint8_t root[32]) {
+    if (!ctx || !root || (n && (!ptrs || !lens))) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    for (uint64_t i = 0; i < n; i++)
+        if (lens[i] && !ptrs[i]) return fail(c, DM_ERR_INVALID, "chunk %llu: NULL pointer", (unsigned long long)i);
+    Dev& d = c->devs[0];
+    RC_TRY(begin_call(c, d, d.stream));
+    std::vector<uint64_t> addr;
+    RC_TRY(pack_chunks(c, d, ptrs, lens, n, addr));
+    RC_TRY(tables_begin(c, d, n * 16 + 1024));
+    HIP_TRY(d.leaves.ensure(n * 32));
+    RC_TRY(upload(c, d, d.stream, d.tab_addr, addr.data(), n * 8));
+    RC_TRY(upload(c, d, d.stream, d.tab_len, lens, n * 8));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(d.tab_addr.p);
+    la.lens = static_cast<const uint64_t*>(d.tab_len.p);
+    la.nleaves = n;
+    la.byte_end = ~0ull;
+    la.digests = d.leaves.u8();
+    hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock), 0,
+                       d.stream, la);
+    HIP_TRY(hipGetLastError());
+    return reduce_leaves_to_host(c, d, n, leaf_out, root);
+}
+
+int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
+                  uint8_t* roots) {
+    if (!ctx || chunk == 0 || (nobj && (!objs || !lens || !roots))) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (nobj == 0) return DM_OK;
+    for (uint64_t o = 0; o < nobj; o++)
+        if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
+    Dev& d = c->devs[0];
+    RC_TRY(begin_call(c, d, d.stream));
+    std::vector<uint64_t> addr;
+    RC_TRY(pack_chunks(c, d, objs, lens, nobj, addr));
+    std::vector<const void*> dptr(nobj);
+    for (uint64_t o = 0; o < nobj; o++) dptr[o] = reinterpret_cast<const void*>(addr[o]);
+    HIP_TRY(d.gather.ensure(nobj * 32));
+    RC_TRY(batch_device(c, d, d.stream, dptr.data(), lens, nobj, chunk, d.gather.u8()));
+    HIP_TRY(hipMemcpyAsync(roots, d.gather.p, nobj * 32, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return DM_OK;
+}
+
+int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t* leaf_out, uint8_t root[32]) {
+    if (!ctx || !root || (n && !paths)) return DM_ERR_INVALID;
+    dm_ctx* c = ctx;
+    if (n == 0) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        return fail(c, DM_ERR_EMPTY, "Empty data");
+    }
+    // types.go:24-35: open and read every file whole, in order; the first error is returned.
+    std::vector<std::vector<uint8_t>> bufs(n);
+    for (uint64_t i = 0; i < n; i++) {
+        FILE* f = paths[i] ? std::fopen(paths[i], "rb") : nullptr;
+        if (!f) {
+            std::string m = std::strerror(errno);
+            if (!m.empty()) m[0] = (char)std::tolower((unsigned char)m[0]);
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            return fail(c, DM_ERR_IO, "open %s: %s", paths[i] ? paths[i] : "(null)", m.c_str());
+        }
+        uint8_t tmp[1 << 16];
+        size_t r;
+        while ((r = std::fread(tmp, 1, sizeof tmp, f)) > 0) bufs[i].insert(bufs[i].end(), tmp, tmp + r);
+        const bool bad = std::ferror(f) != 0;
+        std::fclose(f);
+        if (bad) {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            return fail(c, DM_ERR_IO, "read %s: i/o error", paths[i]);
+        }
+    }
+    std::vector<const void*> ptrs(n);
+    std::vector<uint64_t> lens(n);
+    for (uint64_t i = 0; i < n; i++) {
+        ptrs[i] = bufs[i].data();
+        lens[i] = bufs[i].size();
+    }
+    return dm_root_chunks(ctx, ptrs.data(), lens.data(), n, leaf_out, root);
+}
+
+}  // extern "C"

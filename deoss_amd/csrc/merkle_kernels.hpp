@@ -1,0 +1,294 @@
+// merkle_kernels.hpp -- gfx950 kernels of the DeOSS Merkle path (K1 leaf, K2 tree reduce,
+// K3 batched per-object trees, synthetic generator).  Included by merkle_capi.hip only.
+//
+// Reference algorithm: common/hashtree/hashtree.go:23-30 (leaf = SHA-256 of the chunk),
+// common/hashtree/types.go:19-39 (one leaf per chunk), cbergoon/merkletree v0.2.0 (go.mod:10)
+// buildWithContent/buildIntermediate: level rule out[j] = H(in[2j] || in[min(2j+1, n-1)]),
+// repeated until one node remains, at least one level.
+//
+// Device memory formats: chunk bytes as given; every digest / tree node is the canonical
+// 32-byte big-endian SHA-256 output (what Go's h.Sum(nil) returns).  Inside a kernel nodes
+// live as 8 state words (byte swapped once at load / store).
+#pragma once
+#include "sha256_gfx950.hpp"
+
+namespace dm {
+
+constexpr int kBlock = 256;         // threads per workgroup for K1/K2/K3
+constexpr int kLeafFuseMax = 8;     // K1 reduces its 256 leaves by up to 8 levels in LDS
+constexpr int kReduceTile = 512;    // K2 inputs per workgroup (9 levels max)
+
+struct LeafArgs {
+    const uint8_t* base;        // uniform mode: leaf i starts at base + i * pitch
+    uint64_t pitch;
+    uint64_t leaf_len;          // uniform mode: length of leaves 0 .. n-2
+    uint64_t last_len;          // uniform mode: length of leaf n-1
+    const uint64_t* addrs;      // table mode: device address of leaf i
+    const uint64_t* lens;       // table mode: length of leaf i
+    uint64_t nleaves;
+    // stripe (resumable) mode: this launch absorbs bytes [byte_off, byte_end) of every leaf;
+    // leaf data pointers then point at byte byte_off of the leaf.  Single shot: 0 / ~0.
+    uint64_t byte_off;
+    uint64_t byte_end;
+    uint32_t* state;            // 8 words per leaf, in/out between stripes (nullptr: single shot)
+    uint8_t* digests;           // 32 B per leaf (nullptr: not stored)
+    uint8_t* level_out;         // fused mode: nodes after fuse_levels levels
+    uint32_t fuse_levels;       // 0 .. kLeafFuseMax
+};
+
+__device__ __forceinline__ void load_digest(const uint8_t* p, uint32_t (&v)[8]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 x = q[0], y = q[1];
+    v[0] = bswap32(x.x); v[1] = bswap32(x.y); v[2] = bswap32(x.z); v[3] = bswap32(x.w);
+    v[4] = bswap32(y.x); v[5] = bswap32(y.y); v[6] = bswap32(y.z); v[7] = bswap32(y.w);
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* p, const uint32_t (&v)[8]) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(bswap32(v[0]), bswap32(v[1]), bswap32(v[2]), bswap32(v[3]));
+    q[1] = make_uint4(bswap32(v[4]), bswap32(v[5]), bswap32(v[6]), bswap32(v[7]));
+}
+
+// Load one 64-byte block (16 B aligned) as 4 vector loads.
+struct Blk { uint4 q0, q1, q2, q3; };
+
+template <bool ALIGNED>
+__device__ __forceinline__ Blk load_block(const uint8_t* p) {
+    Blk b;
+    if constexpr (ALIGNED) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+        b.q0 = q[0]; b.q1 = q[1]; b.q2 = q[2]; b.q3 = q[3];
+    } else {
+        __builtin_memcpy(&b, p, 64);
+    }
+    return b;
+}
+
+__device__ __forceinline__ void block_words(const Blk& b, uint32_t (&w)[16]) {
+    w[0] = bswap32(b.q0.x);  w[1] = bswap32(b.q0.y);  w[2] = bswap32(b.q0.z);  w[3] = bswap32(b.q0.w);
+    w[4] = bswap32(b.q1.x);  w[5] = bswap32(b.q1.y);  w[6] = bswap32(b.q1.z);  w[7] = bswap32(b.q1.w);
+    w[8] = bswap32(b.q2.x);  w[9] = bswap32(b.q2.y);  w[10] = bswap32(b.q2.z); w[11] = bswap32(b.q2.w);
+    w[12] = bswap32(b.q3.x); w[13] = bswap32(b.q3.y); w[14] = bswap32(b.q3.z); w[15] = bswap32(b.q3.w);
+}
+
+// Absorb nb full blocks starting at p, one block of loads in flight ahead of the compression.
+template <bool ALIGNED>
+__device__ __forceinline__ void absorb_blocks(uint32_t (&st)[8], const uint8_t* p, uint64_t nb) {
+    if (nb == 0) return;
+    Blk cur = load_block<ALIGNED>(p);
+    for (uint64_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+        block_words(cur, w);
+        if (b + 1 < nb) cur = load_block<ALIGNED>(p + 64 * (b + 1));
+        compress(st, w);
+    }
+}
+
+// FIPS 180-4 padding of the final r (< 64) bytes at p, total message length len bytes.
+template <bool ALIGNED>
+__device__ __forceinline__ void absorb_tail(uint32_t (&st)[8], const uint8_t* p, uint32_t r, uint64_t len) {
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        uint32_t v = 0;
+        if ((uint32_t)(4 * k + 4) <= r) {
+            if constexpr (ALIGNED) {
+                v = bswap32(*reinterpret_cast<const uint32_t*>(p + 4 * k));
+            } else {
+                v = ((uint32_t)p[4 * k] << 24) | ((uint32_t)p[4 * k + 1] << 16) |
+                    ((uint32_t)p[4 * k + 2] << 8) | (uint32_t)p[4 * k + 3];
+            }
+        } else if ((uint32_t)(4 * k) <= r) {
+            // word holding the 0x80 terminator (and 0..3 message bytes)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                uint32_t idx = 4 * k + j;
+                uint32_t byte = idx < r ? (uint32_t)p[idx] : (idx == r ? 0x80u : 0u);
+                v |= byte << (24 - 8 * j);
+            }
+        }
+        w[k] = v;
+    }
+    const uint64_t bits = len * 8;
+    if (r <= 55) {
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(st, w);
+    } else {
+        compress(st, w);
+#pragma unroll
+        for (int k = 0; k < 14; k++) w[k] = 0;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+        compress(st, w);
+    }
+}
+
+// Reduce `cnt` nodes held in LDS (state words, buffer a) for `levels` levels with the
+// merkletree rule; ping-pongs between a and b.  Every thread of the block must call this.
+// Returns the final node count; the result lives in *res.
+__device__ __forceinline__ uint32_t lds_reduce(uint32_t (*a)[8], uint32_t (*b)[8], uint32_t cnt,
+                                               uint32_t levels, uint32_t (**res)[8]) {
+    const uint32_t t = threadIdx.x;
+    for (uint32_t l = 0; l < levels; l++) {
+        const uint32_t next = (cnt + 1) >> 1;
+        if (t < next) {
+            uint32_t L[8], R[8], o[8];
+            const uint32_t ri = (2 * t + 1 < cnt) ? 2 * t + 1 : cnt - 1;
+#pragma unroll
+            for (int k = 0; k < 8; k++) { L[k] = a[2 * t][k]; R[k] = a[ri][k]; }
+            node_hash(L, R, o);
+#pragma unroll
+            for (int k = 0; k < 8; k++) b[t][k] = o[k];
+        }
+        __syncthreads();
+        uint32_t (*tmp)[8] = a; a = b; b = tmp;
+        cnt = next;
+    }
+    *res = a;
+    return cnt;
+}
+
+// K1: leaf SHA-256, one lane per leaf; optionally fused with the first tree levels.
+template <bool TABLE, bool ALIGNED>
+__global__ __launch_bounds__(kBlock) void leaf_kernel(LeafArgs a) {
+    __shared__ uint32_t lds_a[kBlock][8];
+    __shared__ uint32_t lds_b[kBlock / 2][8];
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool active = i < a.nleaves;
+    uint32_t st[8];
+    if (active) {
+        const uint8_t* p;
+        uint64_t len;
+        if constexpr (TABLE) {
+            p = reinterpret_cast<const uint8_t*>(a.addrs[i]);
+            len = a.lens[i];
+        } else {
+            p = a.base + i * a.pitch;
+            len = (i + 1 == a.nleaves) ? a.last_len : a.leaf_len;
+        }
+        // bytes of this leaf inside the stripe [byte_off, byte_end)
+        const uint64_t b0 = a.byte_off;
+        const uint64_t end = len < a.byte_end ? len : a.byte_end;
+        const uint64_t have = end > b0 ? end - b0 : 0;
+        const bool finalize = (b0 < len && len <= a.byte_end) || (len == 0 && b0 == 0);
+        if (a.state != nullptr && b0 != 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) st[k] = a.state[i * 8 + k];
+        } else {
+            init_state(st);
+        }
+        const uint64_t nb = finalize ? have / 64 : have / 64;
+        absorb_blocks<ALIGNED>(st, p, nb);
+        if (finalize) {
+            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(have - 64 * nb), len);
+            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+        } else if (a.state != nullptr && have != 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) a.state[i * 8 + k] = st[k];
+        }
+    }
+    if (a.fuse_levels == 0) return;   // uniform across the grid
+    const uint64_t first = (uint64_t)blockIdx.x * kBlock;
+    const uint32_t cnt = (uint32_t)((a.nleaves - first) < kBlock ? (a.nleaves - first) : kBlock);
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) lds_a[threadIdx.x][k] = st[k];
+    }
+    __syncthreads();
+    uint32_t (*res)[8];
+    const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
+    if (threadIdx.x < out_cnt) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = res[threadIdx.x][k];
+        const uint64_t o = (uint64_t)blockIdx.x * (kBlock >> a.fuse_levels) + threadIdx.x;
+        store_digest(a.level_out + 32 * o, v);
+    }
+}
+
+// K2: tree reduce, `levels` (1..9) levels over tiles of 512 input nodes; the first level reads
+// global memory directly, the rest run in LDS.  Output: ceil(m / 2^levels) nodes.
+__global__ __launch_bounds__(kBlock) void reduce_kernel(const uint8_t* in, uint64_t m, uint32_t levels,
+                                                         uint8_t* out) {
+    __shared__ uint32_t lds_a[kBlock][8];
+    __shared__ uint32_t lds_b[kBlock / 2][8];
+    const uint64_t base = (uint64_t)blockIdx.x * kReduceTile;
+    const uint32_t cnt = (uint32_t)((m - base) < kReduceTile ? (m - base) : kReduceTile);
+    const uint32_t t = threadIdx.x;
+    const uint32_t next = (cnt + 1) >> 1;
+    if (t < next) {
+        uint32_t L[8], R[8], o[8];
+        const uint32_t ri = (2 * t + 1 < cnt) ? 2 * t + 1 : cnt - 1;
+        load_digest(in + 32 * (base + 2 * t), L);
+        load_digest(in + 32 * (base + ri), R);
+        node_hash(L, R, o);
+#pragma unroll
+        for (int k = 0; k < 8; k++) lds_a[t][k] = o[k];
+    }
+    __syncthreads();
+    uint32_t (*res)[8];
+    const uint32_t out_cnt = lds_reduce(lds_a, lds_b, next, levels - 1, &res);
+    if (t < out_cnt) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = res[t][k];
+        store_digest(out + 32 * ((uint64_t)blockIdx.x * (kReduceTile >> levels) + t), v);
+    }
+}
+
+// K3: one workgroup per object, objects of <= 512 leaves: full tree to the root (>= 1 level).
+// leaf_first[o] .. leaf_first[o+1] index the object's leaf digests.
+__global__ __launch_bounds__(kBlock) void batch_root_kernel(const uint8_t* leaves, const uint64_t* leaf_first,
+                                                             const uint32_t* obj_ids, uint8_t* roots) {
+    __shared__ uint32_t lds_a[kBlock][8];
+    __shared__ uint32_t lds_b[kBlock / 2][8];
+    const uint32_t o = obj_ids[blockIdx.x];
+    const uint64_t base = leaf_first[o];
+    const uint32_t cnt = (uint32_t)(leaf_first[o + 1] - base);
+    const uint32_t t = threadIdx.x;
+    const uint32_t next = (cnt + 1) >> 1;
+    if (t < next) {
+        uint32_t L[8], R[8], h[8];
+        const uint32_t ri = (2 * t + 1 < cnt) ? 2 * t + 1 : cnt - 1;
+        load_digest(leaves + 32 * (base + 2 * t), L);
+        load_digest(leaves + 32 * (base + ri), R);
+        node_hash(L, R, h);
+#pragma unroll
+        for (int k = 0; k < 8; k++) lds_a[t][k] = h[k];
+    }
+    __syncthreads();
+    uint32_t levels = 0;
+    for (uint32_t c = next; c > 1; c = (c + 1) >> 1) levels++;
+    uint32_t (*res)[8];
+    lds_reduce(lds_a, lds_b, next, levels, &res);
+    if (t == 0) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = res[0][k];
+        store_digest(roots + 32 * (uint64_t)o, v);
+    }
+}
+
+// Synthetic object bytes: word[i] = splitmix64(seed ^ i) (same as oracle/merkle_oracle.c).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint64_t* dst, uint64_t word0, uint64_t nwords,
+                                                                uint64_t seed) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 2;
+    for (uint64_t j = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 2; j < nwords; j += stride) {
+        if (j + 1 < nwords) {
+            ulonglong2 v = make_ulonglong2(splitmix64(seed ^ (word0 + j)), splitmix64(seed ^ (word0 + j + 1)));
+            *reinterpret_cast<ulonglong2*>(dst + j) = v;
+        } else {
+            dst[j] = splitmix64(seed ^ (word0 + j));
+        }
+    }
+}
+
+}  // namespace dm

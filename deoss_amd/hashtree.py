@@ -1,0 +1,133 @@
+"""Host-side mirror of DeOSS ``common/hashtree`` backed by the MI355X HIP path.
+
+Mirrors the reference Go API (same names, argument meaning and error behaviour):
+
+* ``NewHashTree(chunkPath)`` -- ``common/hashtree/types.go:19-39``: one leaf per file, each read
+  whole; an empty list fails with ``"Empty data"``; open/read errors are returned as errors.
+  Returns ``(tree, err)`` like the Go function.
+* ``HashTreeContent`` -- ``common/hashtree/hashtree.go:18-35`` (``CalculateHash``, ``Equals``).
+* ``MerkleTree`` / ``Node`` -- the parts of ``cbergoon/merkletree`` v0.2.0 the reference test reads:
+  ``Leafs`` (n entries, n+1 when n is odd: the last leaf duplicated with ``dup=True``),
+  ``MerkleRoot()`` and ``Root``.
+
+Deviation (documented in DESIGN.md): interior nodes are not materialised (the GPU reduces the
+tree in LDS); ``Root.Left``/``Right`` are ``None``.  ``Leafs[i].C.Equals`` compares chunk bytes
+when the content was kept (``keep_content=True``) and digests otherwise.
+
+Additive entry points: ``NewHashTreeFromBuffer(buf, chunkSize)`` (the upload-handler host
+buffer path) and ``NewHashTreesBatch(objects, chunkSize)``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+from ._lib import DeossMerkleError
+from .merkle import MerkleContext
+
+_default_ctx: Optional[MerkleContext] = None
+
+
+def default_context() -> MerkleContext:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = MerkleContext()
+    return _default_ctx
+
+
+class HashTreeContent:
+    """Leaf payload (hashtree.go:18-20).  ``x`` holds the chunk bytes (or None if dropped)."""
+
+    def __init__(self, x: Optional[bytes], digest: Optional[bytes] = None):
+        self.x = x
+        self._digest = digest
+
+    def CalculateHash(self) -> Tuple[Optional[bytes], Optional[Exception]]:
+        """SHA-256 of the chunk (hashtree.go:23-30), computed on the GPU."""
+        if self._digest is not None:
+            return self._digest, None
+        try:
+            leaves, _ = default_context().root_chunks([self.x or b""])
+        except DeossMerkleError as e:
+            return None, e
+        self._digest = leaves[:32]
+        return self._digest, None
+
+    def Equals(self, other: "HashTreeContent") -> Tuple[bool, Optional[Exception]]:
+        """hashtree.go:33-35 compares the contents; without kept bytes, compare digests."""
+        if self.x is not None and other.x is not None:
+            return self.x == other.x, None
+        a, e1 = self.CalculateHash()
+        b, e2 = other.CalculateHash()
+        return a == b, e1 or e2
+
+
+@dataclass
+class Node:
+    Hash: bytes
+    C: Optional[HashTreeContent] = None
+    leaf: bool = False
+    dup: bool = False
+    Left: Optional["Node"] = None
+    Right: Optional["Node"] = None
+
+
+@dataclass
+class MerkleTree:
+    Root: Node
+    Leafs: List[Node] = field(default_factory=list)
+
+    def MerkleRoot(self) -> bytes:
+        return self.Root.Hash
+
+
+def _build(leaf_digests: bytes, root: bytes, contents: Sequence[Optional[bytes]]) -> MerkleTree:
+    n = len(leaf_digests) // 32
+    leafs = [Node(Hash=leaf_digests[32 * i:32 * i + 32], C=HashTreeContent(contents[i], leaf_digests[32 * i:32 * i + 32]),
+                  leaf=True) for i in range(n)]
+    if n % 2 == 1:   # merkletree v0.2.0 buildWithContent: duplicate the last leaf
+        last = leafs[-1]
+        leafs.append(Node(Hash=last.Hash, C=last.C, leaf=True, dup=True))
+    return MerkleTree(Root=Node(Hash=root), Leafs=leafs)
+
+
+def NewHashTree(chunkPath: Sequence[str], ctx: Optional[MerkleContext] = None,
+                keep_content: bool = False) -> Tuple[Optional[MerkleTree], Optional[Exception]]:
+    """types.go:19-39 -- build the tree over whole files, one leaf per file."""
+    if len(chunkPath) == 0:
+        return None, DeossMerkleError(-1, "Empty data")
+    c = ctx or default_context()
+    try:
+        leaves, root = c.new_hash_tree(list(chunkPath))
+    except DeossMerkleError as e:
+        return None, e
+    contents: List[Optional[bytes]] = [None] * len(chunkPath)
+    if keep_content:
+        for i, p in enumerate(chunkPath):
+            with open(p, "rb") as f:
+                contents[i] = f.read()
+    return _build(b"".join(leaves), root, contents), None
+
+
+def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContext] = None
+                          ) -> Tuple[Optional[MerkleTree], Optional[Exception]]:
+    """Additive: the object buffer split into chunkSize chunks (last one short)."""
+    if len(buf) == 0:
+        return None, DeossMerkleError(-1, "Empty data")
+    c = ctx or default_context()
+    try:
+        leaves, root = c.root_buffer(buf, chunkSize, want_leaves=True)
+    except DeossMerkleError as e:
+        return None, e
+    n = len(leaves) // 32
+    return _build(leaves, root, [None] * n), None
+
+
+def NewHashTreesBatch(objects: Sequence[bytes], chunkSize: int, ctx: Optional[MerkleContext] = None
+                      ) -> Tuple[Optional[List[bytes]], Optional[Exception]]:
+    """Additive: many independent objects, one root each."""
+    c = ctx or default_context()
+    try:
+        return c.root_batch(list(objects), chunkSize), None
+    except DeossMerkleError as e:
+        return None, e

@@ -1,0 +1,167 @@
+"""Python host binding of the MI355X Merkle path (ctypes over include/deoss_merkle.h).
+
+:class:`MerkleContext` owns a ``dm_ctx`` (one or more GPUs of this process) and exposes the
+C-ABI entry points with Python types.  Device-resident entry points take raw device pointers
+(ints) and a HIP stream handle, so they can be driven from ``torch`` tensors
+(``t.data_ptr()``, ``torch.cuda.current_stream().cuda_stream``) without any torch type crossing
+the boundary.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+from ._lib import DM_ERR_EMPTY, DeossMerkleError, load_library
+
+
+class MerkleContext:
+    def __init__(self, devices: Optional[Sequence[int]] = None):
+        self._L = load_library()
+        h = ctypes.c_void_p()
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = self._L.dm_create(ctypes.byref(h), arr, len(devices))
+        else:
+            rc = self._L.dm_create(ctypes.byref(h), None, 0)
+        if rc != 0:
+            raise DeossMerkleError(rc, f"dm_create: {self._L.dm_strerror(rc).decode()}")
+        self._h = h
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.dm_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def device_count(self) -> int:
+        return self._L.dm_device_count(self._h)
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc == 0:
+            return
+        if rc == DM_ERR_EMPTY:
+            raise DeossMerkleError(rc, "Empty data")
+        detail = (self._L.dm_last_error(self._h) or b"").decode()
+        raise DeossMerkleError(rc, f"{what}: {self._L.dm_strerror(rc).decode()}: {detail}")
+
+    # -- host-memory entry points ------------------------------------------------------------
+    def new_hash_tree(self, paths: Sequence[str]) -> Tuple[List[bytes], bytes]:
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[p.encode() for p in paths])
+        leaf = ctypes.create_string_buffer(max(32 * n, 32))
+        root = ctypes.create_string_buffer(32)
+        rc = self._L.dm_new_hash_tree(self._h, arr, n, leaf, root)
+        if rc != 0:
+            if rc == DM_ERR_EMPTY:
+                raise DeossMerkleError(rc, "Empty data")
+            detail = (self._L.dm_last_error(self._h) or b"").decode()
+            raise DeossMerkleError(rc, detail or self._L.dm_strerror(rc).decode())
+        return [leaf.raw[32 * i:32 * i + 32] for i in range(n)], root.raw
+
+    def root_chunks(self, chunks: Sequence[bytes]) -> Tuple[bytes, bytes]:
+        """Returns (n*32 leaf digest bytes, root)."""
+        n = len(chunks)
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_uint64 * max(n, 1))()
+        keep = []
+        for i, c in enumerate(chunks):
+            b = ctypes.create_string_buffer(bytes(c), max(len(c), 1))
+            keep.append(b)
+            ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            lens[i] = len(c)
+        leaf = ctypes.create_string_buffer(max(32 * n, 32))
+        root = ctypes.create_string_buffer(32)
+        self._check(self._L.dm_root_chunks(self._h, ptrs, lens, n, leaf, root), "dm_root_chunks")
+        return leaf.raw[:32 * n], root.raw
+
+    def root_buffer_ptr(self, addr: int, length: int, chunk: int, want_leaves: bool = False
+                        ) -> Tuple[Optional[bytes], bytes]:
+        n = (length + chunk - 1) // chunk if length and chunk else 0
+        leaf = ctypes.create_string_buffer(max(32 * n, 32)) if want_leaves else None
+        root = ctypes.create_string_buffer(32)
+        self._check(self._L.dm_root_buffer(self._h, ctypes.c_void_p(addr), length, chunk, leaf, root),
+                    "dm_root_buffer")
+        return (leaf.raw[:32 * n] if leaf is not None else None), root.raw
+
+    def root_buffer(self, buf: bytes, chunk: int, want_leaves: bool = True) -> Tuple[Optional[bytes], bytes]:
+        b = ctypes.create_string_buffer(bytes(buf), max(len(buf), 1))
+        return self.root_buffer_ptr(ctypes.addressof(b), len(buf), chunk, want_leaves)
+
+    def root_batch(self, objs: Sequence[bytes], chunk: int) -> List[bytes]:
+        n = len(objs)
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_uint64 * max(n, 1))()
+        keep = []
+        for i, o in enumerate(objs):
+            b = ctypes.create_string_buffer(bytes(o), max(len(o), 1))
+            keep.append(b)
+            ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            lens[i] = len(o)
+        roots = ctypes.create_string_buffer(max(32 * n, 32))
+        self._check(self._L.dm_root_batch(self._h, ptrs, lens, n, chunk, roots), "dm_root_batch")
+        return [roots.raw[32 * i:32 * i + 32] for i in range(n)]
+
+    # -- device-resident entry points ---------------------------------------------------------
+    def root_device(self, dev_ptr: int, length: int, chunk: int) -> bytes:
+        root = ctypes.create_string_buffer(32)
+        self._check(self._L.dm_root_device(self._h, ctypes.c_void_p(dev_ptr), length, chunk, root),
+                    "dm_root_device")
+        return root.raw
+
+    def root_device_async(self, dev_ptr: int, length: int, chunk: int, dev_root: int,
+                          dev_leaves: int = 0, stream: int = 0) -> None:
+        self._check(self._L.dm_root_device_async(self._h, ctypes.c_void_p(dev_ptr), length, chunk,
+                                                 ctypes.c_void_p(dev_root), ctypes.c_void_p(dev_leaves or None),
+                                                 ctypes.c_void_p(stream or None)), "dm_root_device_async")
+
+    def subtree_device_async(self, dev_ptr: int, length: int, chunk: int, levels: int, dev_nodes: int,
+                             stream: int = 0) -> int:
+        nout = ctypes.c_uint64()
+        self._check(self._L.dm_subtree_device_async(self._h, ctypes.c_void_p(dev_ptr), length, chunk, levels,
+                                                    ctypes.c_void_p(dev_nodes), ctypes.byref(nout),
+                                                    ctypes.c_void_p(stream or None)), "dm_subtree_device_async")
+        return nout.value
+
+    def finish_device_async(self, dev_nodes: int, n: int, min_one_level: bool, dev_root: int,
+                            stream: int = 0) -> None:
+        self._check(self._L.dm_finish_device_async(self._h, ctypes.c_void_p(dev_nodes), n, int(min_one_level),
+                                                   ctypes.c_void_p(dev_root), ctypes.c_void_p(stream or None)),
+                    "dm_finish_device_async")
+
+    def root_batch_device_async(self, dev_ptrs: Sequence[int], lens: Sequence[int], chunk: int, dev_roots: int,
+                                stream: int = 0) -> None:
+        n = len(dev_ptrs)
+        ptrs = (ctypes.c_void_p * max(n, 1))(*dev_ptrs)
+        ls = (ctypes.c_uint64 * max(n, 1))(*lens)
+        self._check(self._L.dm_root_batch_device_async(self._h, ptrs, ls, n, chunk, ctypes.c_void_p(dev_roots),
+                                                       ctypes.c_void_p(stream or None)),
+                    "dm_root_batch_device_async")
+
+    def fill_synthetic_async(self, dev_ptr: int, off: int, nbytes: int, seed: int, stream: int = 0) -> None:
+        self._check(self._L.dm_fill_synthetic_async(self._h, ctypes.c_void_p(dev_ptr), off, nbytes, seed,
+                                                    ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
+
+    # -- measurement ----------------------------------------------------------------------------
+    def set_timing(self, enable: bool) -> None:
+        self._check(self._L.dm_set_timing(self._h, int(enable)), "dm_set_timing")
+
+    def timing_summary(self) -> Tuple[int, float, float, float]:
+        """(timed calls, sum of K1 ms, sum of whole-call ms, max K1 ms) since set_timing(True)."""
+        n = ctypes.c_uint64()
+        a, b, m = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        self._check(self._L.dm_timing_summary(self._h, ctypes.byref(n), ctypes.byref(a), ctypes.byref(b),
+                                              ctypes.byref(m)), "dm_timing_summary")
+        return n.value, a.value, b.value, m.value

@@ -1,0 +1,122 @@
+/*
+ * deoss_merkle.h -- C ABI of the MI355X-native Merkle content-hashing path.
+ *
+ * Drop-in boundary for DeOSS common/hashtree (reference repo paths):
+ *   func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error)   common/hashtree/types.go:19
+ *   func (t HashTreeContent) CalculateHash() ([]byte, error)              common/hashtree/hashtree.go:23
+ * The Go side binds these symbols through a cgo shim; the root and leaf digests
+ * returned here are bit-identical to merkletree v0.2.0's MerkleRoot() / Leafs[i].Hash.
+ *
+ * Conventions
+ *  - Return codes: DM_OK (0) or a negative DM_ERR_*; dm_strerror() gives the message
+ *    ("Empty data" for DM_ERR_EMPTY, matching common/hashtree/types.go:21), dm_last_error()
+ *    the detailed message of the last failing call on a context.
+ *  - Digests are the canonical 32-byte big-endian SHA-256 output.  Leaf digests are written
+ *    n x 32 bytes in chunk order (leaf_out may be NULL).  merkletree's duplicated last leaf
+ *    for odd n is NOT written (it equals leaf n-1).
+ *  - Ownership: the caller owns every buffer; nothing is retained after return.
+ *  - Threading: a context serialises its calls internally; separate contexts run in parallel.
+ *  - `stream` arguments are hipStream_t values passed as void* (NULL = the context's stream
+ *    on that device).  *_async calls only enqueue work; device outputs are valid once the
+ *    stream has reached that point.
+ *  - Tree rule (merkletree v0.2.0, restated in DESIGN.md): level out[j] = SHA256(in[2j] ||
+ *    in[min(2j+1, n-1)]), repeated until one node remains, at least one level (n = 1 gives
+ *    SHA256(leaf || leaf)).
+ */
+#ifndef DEOSS_MERKLE_H
+#define DEOSS_MERKLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dm_ctx dm_ctx;
+
+enum {
+    DM_OK = 0,
+    DM_ERR_EMPTY = -1,   /* no chunks: "Empty data" (common/hashtree/types.go:20-22) */
+    DM_ERR_INVALID = -2, /* bad argument (NULL pointer, zero chunk size, bad device id, ...) */
+    DM_ERR_HIP = -3,     /* HIP runtime error */
+    DM_ERR_RCCL = -4,    /* RCCL error */
+    DM_ERR_NOMEM = -5,   /* device or pinned-host allocation failed */
+    DM_ERR_IO = -6,      /* file open/read failed (dm_new_hash_tree; types.go:25-32) */
+    DM_ERR_NODEV = -7    /* no usable GPU */
+};
+
+/* Context over one or more GPUs of this process.  devs == NULL/ndev <= 0: device 0 only.
+ * With ndev > 1 the host-buffer entry points shard a single object by aligned chunk ranges
+ * across the devices and gather per-device subtree roots with RCCL (DESIGN.md "C1"). */
+int dm_create(dm_ctx **out, const int *devs, int ndev);
+void dm_destroy(dm_ctx *ctx);
+const char *dm_strerror(int rc);
+const char *dm_last_error(dm_ctx *ctx);
+int dm_device_count(dm_ctx *ctx);
+
+/* ---- host-memory entry points (synchronous) ---------------------------------------------- */
+
+/* NewHashTree(chunkPath) (types.go:19-39): each file is one leaf, read whole. */
+int dm_new_hash_tree(dm_ctx *ctx, const char *const *paths, uint64_t n, uint8_t *leaf_out,
+                     uint8_t root[32]);
+
+/* Same tree over in-memory chunks (one leaf per chunk, arbitrary lengths, 0 allowed). */
+int dm_root_chunks(dm_ctx *ctx, const void *const *ptrs, const uint64_t *lens, uint64_t n,
+                   uint8_t *leaf_out, uint8_t root[32]);
+
+/* One object buffer split into fixed-size chunks (the last one short): the upload-handler
+ * path (host buffer -> pinned staging -> H2D overlapped with leaf hashing -> root). */
+int dm_root_buffer(dm_ctx *ctx, const void *host, uint64_t len, uint64_t chunk,
+                   uint8_t *leaf_out, uint8_t root[32]);
+
+/* Many independent objects, one root each (roots: nobj x 32 bytes). */
+int dm_root_batch(dm_ctx *ctx, const void *const *objs, const uint64_t *lens, uint64_t nobj,
+                  uint64_t chunk, uint8_t *roots);
+
+/* ---- device-resident entry points ------------------------------------------------------- */
+
+/* Root of an object already in HBM on the context's first device (synchronous). */
+int dm_root_device(dm_ctx *ctx, const void *dev, uint64_t len, uint64_t chunk, uint8_t root[32]);
+
+/* Stream-ordered form: writes the 32-byte root to device memory dev_root.  leaf_out_dev
+ * (nullable) receives n x 32 bytes of leaf digests. */
+int dm_root_device_async(dm_ctx *ctx, const void *dev, uint64_t len, uint64_t chunk,
+                         void *dev_root, void *leaf_out_dev, void *stream);
+
+/* Shard step (multi-GPU, one process per GPU): hash the leaves of a local chunk range and reduce
+ * exactly `levels` levels.  The range must start at a global leaf index that is a multiple of
+ * 2^levels; only the globally last range may end in a short chunk or a partial block.
+ * Writes ceil(nleaves / 2^levels) nodes (32 B each) to dev_nodes and their count to *n_out. */
+int dm_subtree_device_async(dm_ctx *ctx, const void *dev, uint64_t len, uint64_t chunk,
+                            uint32_t levels, void *dev_nodes, uint64_t *n_out, void *stream);
+
+/* Final levels: reduce n nodes (32 B each, device memory) to the root with the tree rule.
+ * min_one_level != 0 forces at least one level (use when the nodes are leaves). */
+int dm_finish_device_async(dm_ctx *ctx, const void *dev_nodes, uint64_t n, int min_one_level,
+                           void *dev_root, void *stream);
+
+/* Batched objects already in HBM: dev_objs[i] (device pointers, host array) of lens[i] bytes.
+ * Writes nobj x 32 bytes of roots to dev_roots. */
+int dm_root_batch_device_async(dm_ctx *ctx, const void *const *dev_objs, const uint64_t *lens,
+                               uint64_t nobj, uint64_t chunk, void *dev_roots, void *stream);
+
+/* Synthetic object bytes: word[i] = splitmix64(seed ^ i) over bytes [off, off+nbytes) of the
+ * object stream, written to dev (off and nbytes multiples of 8). */
+int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbytes, uint64_t seed,
+                            void *stream);
+
+/* ---- measurement ------------------------------------------------------------------------- */
+
+/* Enable (and reset) HIP-event timing: every later call that launches the leaf kernel (K1)
+ * records events on its launch stream around K1 and around the whole call, with no host sync. */
+int dm_set_timing(dm_ctx *ctx, int enable);
+/* Waits for the recorded events and returns: number of timed calls, sum of K1 durations (ms),
+ * sum of whole-call durations (ms), longest K1 duration (ms). */
+int dm_timing_summary(dm_ctx *ctx, uint64_t *ncalls, double *leaf_ms_sum, double *total_ms_sum,
+                      double *leaf_ms_max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DEOSS_MERKLE_H */

@@ -1,0 +1,183 @@
+"""CPU oracle for the DeOSS ``common/hashtree`` Merkle path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker (or the baseline being timed).  The product package
+``deoss_amd`` never imports it.
+
+Two restatements of the same algorithm live here:
+
+* ``py_*``: pure Python over :mod:`hashlib` (OpenSSL FIPS 180-4 SHA-256, standing in for Go's
+  ``crypto/sha256``).  Slow; used for small cases and to generate ``tests/golden`` fixtures.
+* ``Oracle``: ctypes binding of ``oracle/merkle_oracle.c`` (scalar or SHA-NI SHA-256), fast
+  enough for the full-size CPU baseline.
+
+Reference semantics followed (paths relative to the reference repo):
+
+* ``common/hashtree/hashtree.go:23-30`` -- leaf = SHA-256(chunk bytes).
+* ``common/hashtree/types.go:19-39``    -- one leaf per chunk; empty list -> ``"Empty data"``.
+* ``cbergoon/merkletree v0.2.0`` (``go.mod:10``; not vendored, restated) -- odd leaf count
+  duplicates the last leaf; each level pairs (i, i+1) or (i, i) for a trailing odd node;
+  node = SHA-256(left || right); stops at one node, after at least one level.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+from typing import List, Optional, Sequence, Tuple
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle_merkle.so")
+
+
+def py_sha256(b: bytes) -> bytes:
+    return hashlib.sha256(b).digest()
+
+
+def py_level(nodes: Sequence[bytes]) -> List[bytes]:
+    """One merkletree v0.2.0 ``buildIntermediate`` level (right = i when i+1 == len)."""
+    n = len(nodes)
+    return [py_sha256(nodes[2 * j] + nodes[min(2 * j + 1, n - 1)]) for j in range((n + 1) // 2)]
+
+
+def py_reduce(digests: Sequence[bytes], levels: int = -1) -> List[bytes]:
+    """Reduce for exactly ``levels`` levels, or (levels=-1) to one node with at least one level."""
+    cur = list(digests)
+    done = 0
+    while True:
+        if levels >= 0 and done >= levels:
+            break
+        if levels < 0 and done >= 1 and len(cur) == 1:
+            break
+        cur = py_level(cur)
+        done += 1
+    return cur
+
+
+def py_go_tree(chunks: Sequence[bytes]) -> Tuple[List[bytes], bytes]:
+    """Literal restatement of merkletree v0.2.0 NewTree: returns (Leafs hashes incl. dup, root).
+
+    buildWithContent appends a duplicate of the last leaf when the count is odd; buildIntermediate
+    recurses until a level has exactly two nodes and returns their parent.
+    """
+    if len(chunks) == 0:
+        raise ValueError("Empty data")
+    leafs = [py_sha256(c) for c in chunks]
+    if len(leafs) % 2 == 1:
+        leafs.append(leafs[-1])
+    nl = list(leafs)
+    while True:
+        nodes = []
+        for i in range(0, len(nl), 2):
+            left, right = i, i + 1
+            if i + 1 == len(nl):
+                right = i
+            h = py_sha256(nl[left] + nl[right])
+            nodes.append(h)
+            if len(nl) == 2:
+                return leafs, h
+        nl = nodes
+
+
+def py_root_chunks(chunks: Sequence[bytes]) -> Tuple[List[bytes], bytes]:
+    if len(chunks) == 0:
+        raise ValueError("Empty data")
+    leaves = [py_sha256(c) for c in chunks]
+    return leaves, py_reduce(leaves)[0]
+
+
+def split_chunks(buf: bytes, chunk: int) -> List[bytes]:
+    return [buf[i:i + chunk] for i in range(0, len(buf), chunk)]
+
+
+def splitmix64_bytes(nbytes: int, seed: int, off: int = 0) -> bytes:
+    """Synthetic object bytes (numpy): word[i] = splitmix64(seed ^ i), little-endian."""
+    import numpy as np
+    assert off % 8 == 0
+    nw = (nbytes + 7) // 8
+    i = np.arange(off // 8, off // 8 + nw, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) ^ i) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").tobytes()[:nbytes]
+
+
+class Oracle:
+    """ctypes binding of oracle/merkle_oracle.c."""
+
+    def __init__(self, path: str = LIB_PATH):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle` (or __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        u64, vp, cp = ctypes.c_uint64, ctypes.c_void_p, ctypes.c_char_p
+        L.or_sha256.argtypes = [vp, u64, vp]
+        L.or_reduce.argtypes = [vp, u64, ctypes.c_int, vp]
+        L.or_reduce.restype = u64
+        L.or_root_chunks.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(u64), u64, vp, vp, ctypes.c_int]
+        L.or_root_buffer.argtypes = [vp, u64, u64, vp, vp, ctypes.c_int]
+        L.or_fill_splitmix.argtypes = [vp, u64, u64, u64]
+        L.or_set_backend.argtypes = [ctypes.c_int]
+        self.L = L
+
+    def backend(self) -> str:
+        return {1: "scalar", 2: "sha-ni"}[self.L.or_backend()]
+
+    def set_backend(self, name: str) -> None:
+        self.L.or_set_backend({"auto": 0, "scalar": 1, "sha-ni": 0}[name])
+
+    def sha256(self, b: bytes) -> bytes:
+        out = ctypes.create_string_buffer(32)
+        self.L.or_sha256(b, len(b), out)
+        return out.raw
+
+    def reduce(self, digests: bytes, levels: int = -1) -> bytes:
+        n = len(digests) // 32
+        out = ctypes.create_string_buffer(max(32 * n, 32))
+        m = self.L.or_reduce(digests, n, levels, out)
+        return out.raw[:32 * m]
+
+    def root_chunks(self, chunks: Sequence[bytes], nthreads: int = 1) -> Tuple[bytes, bytes]:
+        n = len(chunks)
+        ptrs = (ctypes.c_void_p * max(n, 1))()
+        lens = (ctypes.c_uint64 * max(n, 1))()
+        keep = []
+        for i, c in enumerate(chunks):
+            b = ctypes.create_string_buffer(bytes(c), max(len(c), 1))
+            keep.append(b)
+            ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            lens[i] = len(c)
+        leaf = ctypes.create_string_buffer(max(32 * n, 32))
+        root = ctypes.create_string_buffer(32)
+        rc = self.L.or_root_chunks(ptrs, lens, n, leaf, root, nthreads)
+        if rc == -1:
+            raise ValueError("Empty data")
+        return leaf.raw[:32 * n], root.raw
+
+    def root_buffer_ptr(self, addr: int, length: int, chunk: int, nthreads: int = 1,
+                        want_leaves: bool = False) -> Tuple[Optional[bytes], bytes]:
+        n = (length + chunk - 1) // chunk if length else 0
+        leaf = ctypes.create_string_buffer(max(32 * n, 32)) if want_leaves else None
+        root = ctypes.create_string_buffer(32)
+        rc = self.L.or_root_buffer(ctypes.c_void_p(addr), length, chunk, leaf, root, nthreads)
+        if rc == -1:
+            raise ValueError("Empty data")
+        if rc != 0:
+            raise ValueError(f"or_root_buffer rc={rc}")
+        return (leaf.raw[:32 * n] if leaf is not None else None), root.raw
+
+    def root_buffer(self, buf: bytes, chunk: int, nthreads: int = 1) -> Tuple[bytes, bytes]:
+        b = ctypes.create_string_buffer(bytes(buf), max(len(buf), 1))
+        leaves, root = self.root_buffer_ptr(ctypes.addressof(b), len(buf), chunk, nthreads, True)
+        return leaves, root
+
+    def fill_splitmix_ptr(self, addr: int, off: int, nbytes: int, seed: int) -> None:
+        assert off % 8 == 0 and nbytes % 8 == 0
+        self.L.or_fill_splitmix(ctypes.c_void_p(addr), off, nbytes, seed)
+
+    def splitmix_bytes(self, nbytes: int, seed: int, off: int = 0) -> bytes:
+        n8 = (nbytes + 7) // 8 * 8
+        b = ctypes.create_string_buffer(max(n8, 8))
+        self.fill_splitmix_ptr(ctypes.addressof(b), off, n8, seed)
+        return b.raw[:nbytes]

@@ -1,0 +1,68 @@
+"""CPU checks of the C-ABI boundary: the library loads and exports exactly what the header declares.
+
+No compute calls here (this container has no GPU); the -m gpu tests exercise every entry point.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "deoss_merkle.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(dm_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from deoss_amd import build as b
+    b.build(verbose=False)
+    from deoss_amd import load_library
+    return load_library()
+
+
+def test_header_matches_python_exports():
+    from deoss_amd._lib import EXPORTS
+    assert header_functions() == sorted(EXPORTS)
+
+
+def test_library_exports_every_header_symbol(lib):
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "deoss_amd", "libdeoss_merkle.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (dm_[a-z0-9_]+)$", out, flags=re.M))
+    assert exported == set(header_functions())
+    # the product never links the CPU oracle
+    assert " or_" not in out
+
+
+def test_strerror_messages(lib):
+    assert lib.dm_strerror(0) == b"ok"
+    assert lib.dm_strerror(-1) == b"Empty data"   # common/hashtree/types.go:21
+    assert lib.dm_strerror(-7) == b"no usable GPU"
+
+
+def test_library_is_gfx950_code_object():
+    """The fat binary embeds an amdgcn-amd-amdhsa--gfx950 code object (and nothing else)."""
+    data = open(os.path.join(ROOT, "deoss_amd", "libdeoss_merkle.so"), "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-f]+)", data))
+    assert targets == {b"gfx950"}
+
+
+def test_no_gpu_fails_loudly(lib):
+    """Without a visible GPU, dm_create reports DM_ERR_NODEV (no silent CPU path)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    h = ctypes.c_void_p()
+    assert lib.dm_create(ctypes.byref(h), None, 0) == -7
+    from deoss_amd import DeossMerkleError, MerkleContext
+    with pytest.raises(DeossMerkleError):
+        MerkleContext()

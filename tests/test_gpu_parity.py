@@ -1,0 +1,281 @@
+"""GPU parity tests: every C-ABI entry point against the CPU oracle and the golden fixtures.
+
+Bit-exact comparisons only (integer/byte work).  Run on the MI355X box: pytest -m gpu.
+"""
+import ctypes
+import hashlib
+import os
+import threading
+
+import pytest
+
+from oracle import py_root_chunks, split_chunks, splitmix64_bytes
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def dev_bytes(data: bytes, pad: int = 64, offset: int = 0):
+    """Upload bytes into a fresh uint8 tensor at the given byte offset; returns (tensor, ptr)."""
+    torch = _torch()
+    t = torch.zeros(len(data) + pad + offset, dtype=torch.uint8, device="cuda")
+    if data:
+        import numpy as np
+        t[offset:offset + len(data)] = torch.from_numpy(np.frombuffer(data, dtype=np.uint8).copy()).cuda()
+    return t, t.data_ptr() + offset
+
+
+def chunks_of(case):
+    return [c["text"].encode() if "text" in c else splitmix64_bytes(c["len"], c["seed"]) for c in case["chunks"]]
+
+
+def root_dev(ctx, ptr, length, chunk, want_leaves=False):
+    torch = _torch()
+    n = (length + chunk - 1) // chunk
+    r = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    lv = torch.zeros(max(n, 1) * 32, dtype=torch.uint8, device="cuda") if want_leaves else None
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.root_device_async(ptr, length, chunk, r.data_ptr(), lv.data_ptr() if lv is not None else 0, s)
+    torch.cuda.synchronize()
+    return bytes(r.cpu().numpy()), (bytes(lv.cpu().numpy()) if lv is not None else None)
+
+
+# ---------------------------------------------------------------- reference KAT (Go test shape)
+def test_new_hash_tree_reference_kat(tmp_path):
+    """Mirror of common/hashtree/hashtree_test.go:20-82 through the NewHashTree host mirror."""
+    from deoss_amd import NewHashTree
+    contents = ["content_one", "content_two", "content_three", "content_four"]
+    hashes = [hashlib.sha256(c.encode()).digest() for c in contents]
+    five = hashlib.sha256(hashes[0] + hashes[1]).digest()
+    six = hashlib.sha256(hashes[2] + hashes[3]).digest()
+    roothashs = hashlib.sha256(five + six).digest()
+    chunks = []
+    for c in contents:
+        p = tmp_path / c
+        p.write_bytes(c.encode())
+        chunks.append(str(p))
+    mtree, err = NewHashTree(chunks)
+    assert err is None
+    assert len(mtree.Leafs) == 4
+    for i in range(4):
+        assert mtree.Leafs[i].Hash.hex() == hashes[i].hex()
+    assert mtree.MerkleRoot().hex() == roothashs.hex()
+    assert roothashs.hex() == "b513419286835c1e36fa520b86cbf37650db82e73f510f0e6a699cc0505f1151"
+
+
+def test_new_hash_tree_errors_and_dup(tmp_path):
+    from deoss_amd import NewHashTree
+    tree, err = NewHashTree([])
+    assert tree is None and str(err) == "Empty data"
+    tree, err = NewHashTree([str(tmp_path / "missing")])
+    assert tree is None and "no such file or directory" in str(err) and str(tmp_path / "missing") in str(err)
+    paths = []
+    for i, c in enumerate([b"a", b"bb", b"", b"dddd", b"e"]):
+        p = tmp_path / f"f{i}"
+        p.write_bytes(c)
+        paths.append(str(p))
+    tree, err = NewHashTree(paths, keep_content=True)
+    assert err is None
+    assert len(tree.Leafs) == 6 and tree.Leafs[5].dup and tree.Leafs[5].Hash == tree.Leafs[4].Hash
+    assert tree.Leafs[2].Hash == hashlib.sha256(b"").digest()
+    _, want = py_root_chunks([b"a", b"bb", b"", b"dddd", b"e"])
+    assert tree.MerkleRoot() == want
+    eq, e = tree.Leafs[0].C.Equals(tree.Leafs[0].C)
+    assert eq and e is None
+
+
+# ---------------------------------------------------------------- golden fixtures
+def test_golden_chunks(ctx, golden):
+    for case in golden:
+        if case["kind"] != "chunks":
+            continue
+        leaves, root = ctx.root_chunks(chunks_of(case))
+        assert root.hex() == case["root"], case["name"]
+        assert [leaves[32 * i:32 * i + 32].hex() for i in range(len(case["leaves"]))] == case["leaves"], case["name"]
+
+
+def test_golden_buffers_all_paths(ctx, golden):
+    for case in golden:
+        if case["kind"] != "buffer":
+            continue
+        buf = splitmix64_bytes(case["len"], case["seed"])
+        n, chunk = case["n_leaves"], case["chunk"]
+        # host buffer path
+        leaves, root = ctx.root_buffer(buf, chunk, want_leaves=True)
+        assert root.hex() == case["root"], case["name"]
+        if "leaves" in case:
+            assert [leaves[32 * i:32 * i + 32].hex() for i in range(n)] == case["leaves"], case["name"]
+        else:
+            assert hashlib.sha256(leaves).hexdigest() == case["leaves_sha256"], case["name"]
+        # device-resident path, aligned and misaligned object starts
+        for off in (0, 4, 1):
+            t, ptr = dev_bytes(buf, offset=off)
+            r, lv = root_dev(ctx, ptr, len(buf), chunk, want_leaves=True)
+            assert r.hex() == case["root"], (case["name"], off)
+            assert lv[:32 * n] == leaves, (case["name"], off)
+        assert ctx.root_device(ptr, len(buf), chunk).hex() == case["root"]
+
+
+def test_golden_batch(ctx, golden):
+    torch = _torch()
+    for case in golden:
+        if case["kind"] != "batch":
+            continue
+        objs = [splitmix64_bytes(o["len"], o["seed"]) for o in case["objects"]]
+        roots = ctx.root_batch(objs, case["chunk"])
+        assert [r.hex() for r in roots] == case["roots"]
+        keep = [dev_bytes(o) for o in objs]
+        out = torch.zeros(32 * len(objs), dtype=torch.uint8, device="cuda")
+        ctx.root_batch_device_async([p for _, p in keep], [len(o) for o in objs], case["chunk"], out.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = bytes(out.cpu().numpy())
+        assert [got[32 * i:32 * i + 32].hex() for i in range(len(objs))] == case["roots"]
+
+
+# ---------------------------------------------------------------- edge cases
+def test_leaf_counts_sweep(ctx, oracle_lib):
+    """Every n in 1..600 (odd-node duplication at each level, fused K1 tiles + K2 tiles)."""
+    base = splitmix64_bytes(600 * 64, 11)
+    t, ptr = dev_bytes(base)
+    for n in list(range(1, 300)) + [311, 383, 384, 385, 511, 512, 513, 599, 600]:
+        length = n * 64 - (n % 7)      # ragged last chunk for most n
+        _, want = oracle_lib.root_buffer(base[:length], 64)
+        got, _ = root_dev(ctx, ptr, length, 64)
+        assert got == want, n
+
+
+def test_padding_boundaries_device(ctx, oracle_lib):
+    for chunk in (1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 128, 1000, 4096):
+        for length in (1, chunk, chunk + 1, 3 * chunk - 1, 5 * chunk):
+            buf = splitmix64_bytes(length, chunk * 1000 + length)
+            t, ptr = dev_bytes(buf)
+            lw, want = oracle_lib.root_buffer(buf, chunk)
+            got, lv = root_dev(ctx, ptr, length, chunk, want_leaves=True)
+            assert got == want, (chunk, length)
+            assert lv[:len(lw)] == lw
+
+
+def test_many_leaves_multi_stage(ctx, oracle_lib):
+    """> 2^17 leaves: K1 fused 8 levels + two K2 launches (9 + rest)."""
+    torch = _torch()
+    length, chunk = (1 << 18) * 64 + 17, 64
+    buf = torch.empty(length + 64, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, (length + 7) // 8 * 8, 99, torch.cuda.current_stream().cuda_stream)
+    host = oracle_lib.splitmix_bytes(length, 99)
+    torch.cuda.synchronize()
+    assert bytes(buf[:length].cpu().numpy()) == host       # device generator == host generator
+    _, want = oracle_lib.root_buffer(host, chunk, nthreads=8)
+    got, _ = root_dev(ctx, buf.data_ptr(), length, chunk)
+    assert got == want
+
+
+def test_empty_and_invalid(ctx):
+    from deoss_amd import DeossMerkleError
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        ctx.root_chunks([])
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        ctx.root_buffer(b"", 64)
+    with pytest.raises(DeossMerkleError):
+        ctx.root_buffer(b"abc", 0)
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        ctx.root_batch([b"x", b""], 64)
+
+
+# ---------------------------------------------------------------- sharding (subtree + finish)
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
+def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world):
+    """The multi-GPU decomposition (deoss_amd.sharding) on one device: per-rank subtree to k
+    levels on each rank's byte range, concatenate, finish == the single-object root."""
+    torch = _torch()
+    from deoss_amd import plan_shards
+    s = torch.cuda.current_stream().cuda_stream
+    for length, chunk in [(1000 * 4096 + 5, 4096), (64 * 1024, 1024), (37 * 512, 512), (5 * 64, 64), (3000, 1000)]:
+        host = oracle_lib.splitmix_bytes(length, length)
+        _, want = oracle_lib.root_buffer(host, chunk)
+        t, ptr = dev_bytes(host)
+        plan = plan_shards(length, chunk, world)
+        parts = []
+        for r in range(world):
+            b0, b1 = plan.byte_range(r)
+            if b1 <= b0:
+                continue
+            nodes = torch.zeros(plan.node_count(r) * 32, dtype=torch.uint8, device="cuda")
+            cnt = ctx.subtree_device_async(ptr + b0, b1 - b0, chunk, plan.k, nodes.data_ptr(), s)
+            assert cnt == plan.node_count(r)
+            parts.append(nodes)
+        allnodes = torch.cat(parts)
+        root = torch.zeros(32, dtype=torch.uint8, device="cuda")
+        ctx.finish_device_async(allnodes.data_ptr(), plan.n_blocks, plan.k == 0, root.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert bytes(root.cpu().numpy()) == want, (length, chunk, world)
+
+
+# ---------------------------------------------------------------- host buffer e2e (stripes)
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_buffer_striped_large_leaves(ctx, oracle_lib, pinned):
+    """Few large leaves (> 256 MiB object): the striped H2D path with resumable leaf state."""
+    torch = _torch()
+    length, chunk = (300 << 20) + 12345, 64 << 20
+    t = torch.empty(length, dtype=torch.uint8, pin_memory=pinned)
+    oracle_lib.fill_splitmix_ptr(t.data_ptr(), 0, length // 8 * 8, 5)
+    leaves_want, want = oracle_lib.root_buffer_ptr(t.data_ptr(), length, chunk, nthreads=8, want_leaves=True)
+    leaves, root = ctx.root_buffer_ptr(t.data_ptr(), length, chunk, want_leaves=True)
+    assert root == want and leaves == leaves_want
+
+
+def test_host_buffer_many_leaves(ctx, oracle_lib):
+    torch = _torch()
+    length, chunk = (96 << 20) + 3, 16 << 10
+    t = torch.empty(length, dtype=torch.uint8)
+    oracle_lib.fill_splitmix_ptr(t.data_ptr(), 0, length // 8 * 8, 6)
+    _, want = oracle_lib.root_buffer_ptr(t.data_ptr(), length, chunk, nthreads=8)
+    _, root = ctx.root_buffer_ptr(t.data_ptr(), length, chunk)
+    assert root == want
+
+
+# ---------------------------------------------------------------- concurrency (gin handlers)
+def test_concurrent_callers(ctx, oracle_lib):
+    """Several host threads share one context (calls serialise inside) plus private contexts."""
+    from deoss_amd import MerkleContext
+    bufs = [splitmix64_bytes(200000 + 977 * i, 300 + i) for i in range(8)]
+    wants = [oracle_lib.root_buffer(b, 4096)[1] for b in bufs]
+    got = [None] * len(bufs)
+    errors = []
+
+    def worker(i):
+        try:
+            if i % 2:
+                got[i] = ctx.root_buffer(bufs[i], 4096, want_leaves=False)[1]
+            else:
+                with MerkleContext() as c2:
+                    got[i] = c2.root_buffer(bufs[i], 4096, want_leaves=False)[1]
+        except Exception as e:   # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(bufs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors
+    assert got == wants
+
+
+def test_timing_events(ctx):
+    torch = _torch()
+    buf = torch.empty(64 << 20, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, buf.numel(), 1, s)
+    ctx.set_timing(True)
+    r = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    ctx.root_device_async(buf.data_ptr(), buf.numel(), 64 << 10, r.data_ptr(), 0, s)
+    ctx.root_device_async(buf.data_ptr(), buf.numel(), 64 << 10, r.data_ptr(), 0, s)
+    n, leaf_ms, total_ms, mx = ctx.timing_summary()
+    ctx.set_timing(False)
+    assert n == 2 and 0 < leaf_ms <= total_ms and 0 < mx <= leaf_ms

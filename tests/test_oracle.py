@@ -1,0 +1,134 @@
+"""CPU tests pinning the oracle (oracle/) before it is trusted as the GPU checker."""
+import hashlib
+import random
+
+import pytest
+
+from oracle import (py_go_tree, py_reduce, py_root_chunks, split_chunks, splitmix64_bytes)
+
+
+def chunks_of(case):
+    out = []
+    for c in case["chunks"]:
+        out.append(c["text"].encode() if "text" in c else splitmix64_bytes(c["len"], c["seed"]))
+    return out
+
+
+# NIST FIPS 180-4 / CSRC example vectors for SHA-256
+NIST = [
+    (b"", "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"),
+    (b"abc", "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"),
+    (b"abcdefghbcdefghicdefghijdefghijkefghijklfghijklmghijklmnhijklmnoijklmnopjklmnopqklmnopqrlmnopqrsmnopqrstnopqrstu",
+     "cf5b16a778af8380036ce59e7b0492370b249b11e8f07a51afac45037afee9d1"),
+    (b"a" * 1000000, "cdc76e5c9914fb9281a1c7e284d73e67f1809a48a497200e046d39ccc7112cd0"),
+]
+
+
+@pytest.mark.parametrize("backend", ["scalar", "sha-ni"])
+def test_nist_vectors(oracle_lib, backend):
+    if backend == "sha-ni" and oracle_lib.backend() != "sha-ni":
+        pytest.skip("CPU has no SHA-NI")
+    oracle_lib.set_backend(backend)
+    try:
+        for msg, want in NIST:
+            assert oracle_lib.sha256(msg).hex() == want
+            assert hashlib.sha256(msg).hexdigest() == want
+    finally:
+        oracle_lib.set_backend("auto")
+
+
+def test_reference_kat(oracle_lib):
+    """common/hashtree/hashtree_test.go:20-82, expected root built exactly as the Go test does."""
+    texts = [b"content_one", b"content_two", b"content_three", b"content_four"]
+    L = [hashlib.sha256(t).digest() for t in texts]
+    want_root = hashlib.sha256(hashlib.sha256(L[0] + L[1]).digest() + hashlib.sha256(L[2] + L[3]).digest()).digest()
+    assert want_root.hex() == "b513419286835c1e36fa520b86cbf37650db82e73f510f0e6a699cc0505f1151"
+    leafs, root = py_go_tree(texts)
+    assert len(leafs) == 4 and leafs == L and root == want_root
+    leaves, root2 = oracle_lib.root_chunks(texts)
+    assert root2 == want_root
+    assert [leaves[32 * i:32 * i + 32] for i in range(4)] == L
+
+
+def test_single_leaf_self_pair():
+    """n = 1: merkletree v0.2.0 duplicates the leaf, root = SHA256(L || L)."""
+    leafs, root = py_go_tree([b"content_one"])
+    assert len(leafs) == 2 and leafs[1] == leafs[0]
+    assert root == hashlib.sha256(leafs[0] + leafs[0]).digest()
+    assert root.hex().startswith("343fcc89") and root.hex().endswith("03b6")
+
+
+def test_go_tree_equals_level_rule():
+    """Literal buildWithContent/buildIntermediate == the min(2j+1, n-1) level rule, n = 1..300."""
+    rnd = random.Random(1)
+    for n in list(range(1, 70)) + [127, 128, 129, 255, 256, 257, 300]:
+        ch = [bytes(rnd.getrandbits(8) for _ in range(rnd.randint(0, 40))) for _ in range(n)]
+        leafs, r1 = py_go_tree(ch)
+        assert len(leafs) == n + (n % 2)
+        _, r2 = py_root_chunks(ch)
+        assert r1 == r2, n
+
+
+def test_reduce_exact_levels_compose():
+    """k levels then the rest == the full reduction (the sharding identity, single process)."""
+    rnd = random.Random(2)
+    for n in (1, 2, 3, 5, 8, 13, 64, 100, 257):
+        leaves = [rnd.randbytes(32) for _ in range(n)]
+        full = py_reduce(leaves)
+        depth = max(1, (n - 1).bit_length())   # levels the full tree needs
+        for k in range(0, depth + 1):
+            part = py_reduce(leaves, k)
+            rest = py_reduce(part) if (k == 0 or len(part) > 1) else part
+            assert rest == full, (n, k)
+
+
+def test_golden_fixtures_match_oracles(golden, oracle_lib):
+    for case in golden:
+        if case["kind"] == "chunks":
+            data = chunks_of(case)
+            leaves, root = py_root_chunks(data)
+            assert root.hex() == case["root"], case["name"]
+            assert [x.hex() for x in leaves] == case["leaves"], case["name"]
+            cl, cr = oracle_lib.root_chunks(data, nthreads=3)
+            assert cr.hex() == case["root"], case["name"]
+            assert cl == b"".join(leaves)
+            if "go_leafs_len" in case:
+                assert case["go_leafs_len"] == len(data) + len(data) % 2
+        elif case["kind"] == "buffer":
+            buf = splitmix64_bytes(case["len"], case["seed"])
+            assert oracle_lib.splitmix_bytes(case["len"], case["seed"]) == buf
+            cl, cr = oracle_lib.root_buffer(buf, case["chunk"], nthreads=4)
+            assert cr.hex() == case["root"], case["name"]
+            assert len(cl) // 32 == case["n_leaves"]
+            if "leaves" in case:
+                assert [cl[32 * i:32 * i + 32].hex() for i in range(case["n_leaves"])] == case["leaves"]
+            else:
+                assert hashlib.sha256(cl).hexdigest() == case["leaves_sha256"]
+        elif case["kind"] == "batch":
+            for o, want in zip(case["objects"], case["roots"]):
+                buf = splitmix64_bytes(o["len"], o["seed"])
+                assert oracle_lib.root_buffer(buf, case["chunk"])[1].hex() == want
+                assert py_root_chunks(split_chunks(buf, case["chunk"]))[1].hex() == want
+
+
+def test_empty_data(oracle_lib):
+    with pytest.raises(ValueError, match="Empty data"):
+        py_go_tree([])
+    with pytest.raises(ValueError, match="Empty data"):
+        oracle_lib.root_chunks([])
+
+
+def test_threaded_equals_serial(oracle_lib):
+    buf = splitmix64_bytes(3 << 20, 77)
+    a = oracle_lib.root_buffer(buf, 4096, nthreads=1)
+    b = oracle_lib.root_buffer(buf, 4096, nthreads=8)
+    assert a == b
+
+
+def test_splitmix_offsets(oracle_lib):
+    full = oracle_lib.splitmix_bytes(1 << 16, 5)
+    part = oracle_lib.splitmix_bytes(1 << 12, 5, off=1 << 15)
+    assert full[1 << 15:(1 << 15) + (1 << 12)] == part
+    assert splitmix64_bytes(1 << 12, 5, off=1 << 15) == part
