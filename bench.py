@@ -22,7 +22,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
-VALU_LANE_OPS_PEAK = 256 * 128 * 2.4e9   # 256 CU x 4 SIMD-32 x 2.4 GHz (int32 lane-ops/s)
+VALU_SLOT_PEAK = 256 * 128 * 2.4e9   # 256 CU x 4 SIMD-32 x 2.4 GHz: full-rate int32 lane-slots/s
 SEED = 0xDE0550002               # configs[1] seed (0xDE0550000 + k)
 
 
@@ -44,14 +44,19 @@ def blocks_for(length: int, chunk: int) -> int:
     return leaf_blocks + 2 * nodes
 
 
-def load_traffic(kernel_hint: str):
-    """PMC HBM bytes per K1 launch from the committed rocprofv3 summary, if present."""
+def load_traffic(n_leaves: int):
+    """PMC HBM bytes per K1 launch for this launch shape, from the committed rocprofv3 passes
+    (profiles/k1_traffic.json, made by tools/pmc_traffic.py from the same bench command)."""
     path = os.path.join(ROOT, "profiles", "k1_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), d
+    grid = str((n_leaves + 255) // 256 * 256)
+    e = d.get("by_grid_threads", {}).get(grid)
+    if not e:
+        return None, None
+    return e["hbm_bytes_per_launch"], "profiles/k1_traffic.json <- " + d.get("source", "")
 
 
 def main() -> None:
@@ -140,8 +145,8 @@ def main() -> None:
     achieved_gbs = k1_bytes / (k1_avg_ms * 1e-3) / 1e9 if k1_avg_ms > 0 else 0.0
     blocks = blocks_for(local_len, chunk)
     from deoss_amd.isa import valu_per_block
-    vpb = valu_per_block()
-    traffic, traffic_src = load_traffic("leaf_kernel")
+    vpb, spb = valu_per_block()
+    traffic, traffic_src = load_traffic((local_len + chunk - 1) // chunk)
 
     out = {
         "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling",
@@ -167,15 +172,16 @@ def main() -> None:
             "bound": "hbm", "kernel": "leaf_kernel (K1)",
             "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
-            "traffic": traffic, "traffic_source": traffic_src.get("source") if traffic_src else None,
+            "traffic": traffic, "traffic_source": traffic_src,
             "k1_avg_ms": round(k1_avg_ms, 4), "k1_launches": ncalls,
             "algorithmic_bytes_per_launch": k1_bytes,
             "valu": {
-                "ops_per_block": vpb, "blocks_per_step": blocks,
-                "achieved_lane_ops_per_s": (blocks * vpb / (k1_avg_ms * 1e-3)) if (vpb and k1_avg_ms) else None,
-                "peak_lane_ops_per_s": VALU_LANE_OPS_PEAK,
-                "frac": (blocks * vpb / (k1_avg_ms * 1e-3) / VALU_LANE_OPS_PEAK) if (vpb and k1_avg_ms) else None,
-                "note": "binding bound for SHA-256 is integer VALU issue, not HBM (DESIGN.md)",
+                "ops_per_block": vpb, "slots_per_block": spb, "blocks_per_step": blocks,
+                "achieved_slots_per_s": (blocks * spb / (k1_avg_ms * 1e-3)) if (spb and k1_avg_ms) else None,
+                "peak_slots_per_s": VALU_SLOT_PEAK,
+                "frac": round(blocks * spb / (k1_avg_ms * 1e-3) / VALU_SLOT_PEAK, 6) if (spb and k1_avg_ms) else None,
+                "note": "SHA-256 is bound by integer VALU issue, not HBM; v_alignbit/v_add3 cost 2 slots "
+                        "(measured, tools/valu_peak.hip); see DESIGN.md",
             },
         },
         "root": root_hex,

@@ -99,6 +99,7 @@ struct Dev {
     hipEvent_t ev_done = nullptr;
     hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_htab = nullptr;
     hipStream_t last_stream = nullptr;  // stream of the last enqueued call (scratch ordering)
+    bool has_last = false;
     // timing records: (K1 begin, K1 end, call end) per timed call, reused across resets
     std::vector<hipEvent_t> tev;
     size_t ntimed = 0;
@@ -147,16 +148,19 @@ int fail(dm_ctx* c, int code, const char* fmt, ...) {
             return fail(c, DM_ERR_RCCL, "%s: %s", #expr, ncclGetErrorString(r_));              \
     } while (0)
 
-hipStream_t pick_stream(Dev& d, void* s) { return s ? static_cast<hipStream_t>(s) : d.stream; }
+// *_async calls run on the caller's stream verbatim: NULL is HIP's null (legacy default) stream,
+// which is also what torch's default stream handle (0) denotes.
+hipStream_t pick_stream(Dev&, void* s) { return static_cast<hipStream_t>(s); }
 
 // Order this call's use of the context scratch after the previous call's (possibly other stream).
 int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
     HIP_TRY(hipSetDevice(d.id));
-    if (d.last_stream != nullptr && d.last_stream != s) {
+    if (d.has_last && d.last_stream != s) {
         HIP_TRY(hipEventRecord(d.ev_done, d.last_stream));
         HIP_TRY(hipStreamWaitEvent(s, d.ev_done, 0));
     }
     d.last_stream = s;
+    d.has_last = true;
     return DM_OK;
 }
 

@@ -71,7 +71,9 @@ __device__ __forceinline__ void block_words(const Blk& b, uint32_t (&w)[16]) {
     w[12] = bswap32(b.q3.x); w[13] = bswap32(b.q3.y); w[14] = bswap32(b.q3.z); w[15] = bswap32(b.q3.w);
 }
 
-// Absorb nb full blocks starting at p, one block of loads in flight ahead of the compression.
+// Absorb nb full blocks starting at p, the next block's loads in flight during each
+// compression (register double buffer).  A paired 128-byte variant was measured to make hipcc
+// sink the prefetch next to its use (DESIGN.md "K1"), so blocks stay 64 bytes per iteration.
 template <bool ALIGNED>
 __device__ __forceinline__ void absorb_blocks(uint32_t (&st)[8], const uint8_t* p, uint64_t nb) {
     if (nb == 0) return;

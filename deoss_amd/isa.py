@@ -14,6 +14,10 @@ import subprocess
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+# Issue slots per wave64 instruction relative to v_add_u32, measured on MI355X by
+# tools/valu_peak.hip (profiles/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
+# the v_add_u32 / v_bitop3_b32 rate.
+SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0}
 COUNTS = os.path.join(HERE, "isa_counts.json")
 K1_SYMBOL = "_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE"
 
@@ -71,7 +75,10 @@ def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
         for x in valu:
             op = x.split()[0]
             hist[op] = hist.get(op, 0) + 1
-        best = {"valu": len(valu), "salu": sum(1 for x in loop if x.startswith("s_")),
+        per = max(1, loads // 4)   # 64-byte blocks per loop iteration
+        slots = sum(SLOT_WEIGHTS.get(x.split()[0], 1.0) for x in valu)
+        best = {"valu": round(len(valu) / per, 1), "valu_slots": round(slots / per, 1), "blocks_per_iteration": per,
+                "valu_per_iteration": len(valu), "salu": sum(1 for x in loop if x.startswith("s_")),
                 "vmem": sum(1 for x in loop if x.startswith(("global_", "buffer_", "flat_"))),
                 "total": len(loop), "valu_histogram": dict(sorted(hist.items(), key=lambda kv: -kv[1]))}
     if best is None:
@@ -96,11 +103,13 @@ def generate() -> dict:
 
 
 def valu_per_block():
+    """(VALU instructions, full-rate issue slots) per 64-byte block of the K1 loop."""
     try:
         with open(COUNTS) as f:
-            return json.load(f)["valu"]
+            d = json.load(f)
+            return d["valu"], d["valu_slots"]
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 if __name__ == "__main__":

@@ -4,7 +4,8 @@
 C-ABI entry points with Python types.  Device-resident entry points take raw device pointers
 (ints) and a HIP stream handle, so they can be driven from ``torch`` tensors
 (``t.data_ptr()``, ``torch.cuda.current_stream().cuda_stream``) without any torch type crossing
-the boundary.
+the boundary.  ``stream=0`` is HIP's null stream (torch's default stream): work is ordered with
+torch's own kernels and copies on that stream.
 """
 from __future__ import annotations
 

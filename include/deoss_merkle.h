@@ -16,9 +16,10 @@
  *    for odd n is NOT written (it equals leaf n-1).
  *  - Ownership: the caller owns every buffer; nothing is retained after return.
  *  - Threading: a context serialises its calls internally; separate contexts run in parallel.
- *  - `stream` arguments are hipStream_t values passed as void* (NULL = the context's stream
- *    on that device).  *_async calls only enqueue work; device outputs are valid once the
- *    stream has reached that point.
+ *  - `stream` arguments are hipStream_t values passed as void*, used verbatim (NULL is HIP's
+ *    null stream, e.g. torch's default stream).  *_async calls only enqueue work on that
+ *    stream; device inputs must be ready in stream order and outputs are valid once the
+ *    stream has reached that point.  Synchronous calls use the context's own streams.
  *  - Tree rule (merkletree v0.2.0, restated in DESIGN.md): level out[j] = SHA256(in[2j] ||
  *    in[min(2j+1, n-1)]), repeated until one node remains, at least one level (n = 1 gives
  *    SHA256(leaf || leaf)).

@@ -1,0 +1,74 @@
+// C++ mirror of the reference test common/hashtree/hashtree_test.go:20-82, through the C++ host
+// API (include/deoss_hashtree.hpp) and the GPU library.  Prints "PASS" and exits 0 on success.
+// Expected digests are computed independently with the CPU oracle's SHA-256 (linked in only as
+// the checker, never by the product library).
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "deoss_hashtree.hpp"
+
+extern "C" void or_sha256(const void* data, uint64_t len, uint8_t out[32]);
+
+static int fails = 0;
+#define EXPECT(c)                                                   \
+    do {                                                            \
+        if (!(c)) {                                                 \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c); \
+            fails++;                                                \
+        }                                                           \
+    } while (0)
+
+static hashtree::Digest sha(const std::string& s) {
+    hashtree::Digest d;
+    or_sha256(s.data(), s.size(), d.data());
+    return d;
+}
+
+int main(int argc, char** argv) {
+    const std::string dir = argc > 1 ? argv[1] : "/tmp";
+    const char* contents[] = {"content_one", "content_two", "content_three", "content_four"};
+    std::vector<std::string> chunks;
+    std::vector<hashtree::Digest> hashes;
+    for (const char* c : contents) {
+        std::string p = dir + "/" + c;
+        FILE* f = std::fopen(p.c_str(), "wb");
+        std::fwrite(c, 1, std::strlen(c), f);
+        std::fclose(f);
+        chunks.push_back(p);
+        hashes.push_back(sha(c));
+    }
+    auto cat = [](const hashtree::Digest& a, const hashtree::Digest& b) {
+        return std::string(reinterpret_cast<const char*>(a.data()), 32) + std::string(reinterpret_cast<const char*>(b.data()), 32);
+    };
+    hashtree::Digest five = sha(cat(hashes[0], hashes[1])), six = sha(cat(hashes[2], hashes[3]));
+    hashtree::Digest root = sha(cat(five, six));
+
+    auto [mtree, err] = hashtree::NewHashTree(chunks);
+    EXPECT(!err.has_value());
+    EXPECT(mtree && mtree->Leafs.size() == 4);
+    for (int i = 0; i < 4 && mtree; i++) EXPECT(mtree->Leafs[i].Hash == hashes[i]);
+    EXPECT(mtree && mtree->MerkleRoot() == root);
+
+    auto [t0, e0] = hashtree::NewHashTree({});
+    EXPECT(!t0 && e0 && e0->message == "Empty data");
+    auto [t1, e1] = hashtree::NewHashTree({dir + "/does_not_exist"});
+    EXPECT(!t1 && e1 && e1->message.find("no such file or directory") != std::string::npos);
+
+    // odd leaf count: Leafs gets the duplicated last leaf
+    std::vector<std::string> three(chunks.begin(), chunks.begin() + 3);
+    auto [t3, e3] = hashtree::NewHashTree(three);
+    EXPECT(!e3 && t3 && t3->Leafs.size() == 4 && t3->Leafs[3].dup && t3->Leafs[3].Hash == hashes[2]);
+    hashtree::Digest h01 = sha(cat(hashes[0], hashes[1])), h22 = sha(cat(hashes[2], hashes[2]));
+    EXPECT(t3 && t3->MerkleRoot() == sha(cat(h01, h22)));
+
+    // buffer entry point
+    std::string obj = "content_onecontent_two";
+    auto [tb, eb] = hashtree::NewHashTreeFromBuffer(obj.data(), obj.size(), 11);
+    EXPECT(!eb && tb && tb->MerkleRoot() == sha(cat(hashes[0], hashes[1])));
+
+    if (fails) return 1;
+    std::printf("PASS\n");
+    return 0;
+}

@@ -279,3 +279,19 @@ def test_timing_events(ctx):
     n, leaf_ms, total_ms, mx = ctx.timing_summary()
     ctx.set_timing(False)
     assert n == 2 and 0 < leaf_ms <= total_ms and 0 < mx <= leaf_ms
+
+
+# ---------------------------------------------------------------- C++ host mirror
+def test_cpp_host_mirror(tmp_path):
+    """Compile and run tests/cpp/test_hashtree.cpp (C++ mirror of hashtree_test.go) on the GPU."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "test_hashtree")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "test_hashtree.cpp"),
+                    "-L", os.path.join(root, "deoss_amd"), "-ldeoss_merkle",
+                    "-L", os.path.join(root, "oracle"), "-loracle_merkle",   # checker's SHA-256 only
+                    "-Wl,-rpath," + os.path.join(root, "deoss_amd") + ":" + os.path.join(root, "oracle"),
+                    "-lpthread", "-o", exe], check=True)
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
