@@ -70,6 +70,8 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
+    ap.add_argument("--sweep-modes", action="store_true", help="sweep both leaf kernels (wide, latency)")
+    ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency"])
     args = ap.parse_args()
 
     import torch
@@ -94,6 +96,7 @@ def main() -> None:
     b0, b1 = plan.byte_range(rank)
     local_len = b1 - b0
     ctx = MerkleContext(devices=[local_rank])
+    ctx.set_leaf_kernel(args.leaf_kernel)
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
     buf = torch.empty(local_len + 64, dtype=torch.uint8, device=device)
@@ -233,7 +236,9 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     if not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
-        for c in [int(x) for x in args.sweep_chunks.split(",")]:
+        modes = ["wide", "latency"] if args.sweep_modes else ["auto"]
+        for c, mode in [(int(x), m) for x in args.sweep_chunks.split(",") for m in modes]:
+            ctx.set_leaf_kernel(mode)
             reps = 3 if c < (8 << 20) else 2
             ctx.root_device_async(buf.data_ptr(), length, c, root.data_ptr(), 0, sptr)
             torch.cuda.synchronize()
@@ -246,7 +251,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
             n, k1, tot, _ = ctx.timing_summary()
             ctx.set_timing(False)
             gpu_root = bytes(root.cpu().numpy())
-            entry = {"chunk": c, "leaves": (length + c - 1) // c,
+            entry = {"chunk": c, "leaves": (length + c - 1) // c, "leaf_kernel": mode,
                      "gibs": round(length * reps / (t1 - t0) / (1 << 30), 3),
                      "k1_gbs": round(length / (k1 / n * 1e-3) / 1e9, 2),
                      "k1_hbm_frac": round(length / (k1 / n * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
@@ -254,6 +259,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
                 _, cr = orc.root_buffer_ptr(host.data_ptr(), length, c, nthreads=min(16, os.cpu_count() or 1))
                 entry["bit_exact"] = cr == gpu_root
             sweep.append(entry)
+        ctx.set_leaf_kernel("auto")
         out["sweep"] = sweep
 
 

@@ -31,6 +31,7 @@ namespace {
 constexpr uint64_t kAlign = 256;                    // leaf start alignment when packing chunks
 constexpr uint64_t kStageBytes = 64ull << 20;       // pinned staging slot
 constexpr uint64_t kStripeBudget = 256ull << 20;    // bytes per H2D stripe / batch (e2e path)
+constexpr uint64_t kLatencyLeafMax = 32768;         // auto mode: K1L up to this many leaves
 
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
@@ -113,6 +114,7 @@ struct dm_ctx {
     std::vector<ncclComm_t> comms;
     std::string err;
     bool timing = false;
+    int leaf_mode = DM_LEAF_AUTO;
 };
 
 namespace {
@@ -224,11 +226,21 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 
 // Hash the leaves described by `la` (uniform or table mode) and reduce `levels` levels
 // (levels < 0: to the root, >= 1 level).  Nodes go to dst; *nout gets their count.
+// Leaf-kernel choice for a uniform-chunk object of n leaves: the producer/consumer latency
+// kernel (K1L) while the leaves cannot fill the chip, the one-lane-per-leaf kernel (K1) after.
+bool use_latency_kernel(const dm_ctx* c, uint64_t n, bool table) {
+    if (table) return false;
+    if (c->leaf_mode == DM_LEAF_WIDE) return false;
+    if (c->leaf_mode == DM_LEAF_LATENCY) return true;
+    return n <= kLatencyLeafMax;
+}
+
 int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool aligned, int levels,
              uint8_t* dst, uint64_t* nout, uint8_t* leaf_dig) {
     const uint64_t n = la.nleaves;
+    const bool lat = use_latency_kernel(c, n, table);
     const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
-    const uint32_t L1 = std::min<uint32_t>(dm::kLeafFuseMax, D);
+    const uint32_t L1 = std::min<uint32_t>(lat ? dm::kLatFuseMax : dm::kLeafFuseMax, D);
     const uint64_t m1 = ceil_shift(n, L1);
     la.byte_off = 0;
     la.byte_end = ~0ull;
@@ -248,13 +260,19 @@ int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool
     }
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
-    if (table) {
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+    if (lat) {
+        const uint32_t grid = (uint32_t)ceil_div(n, dm::kLatLeaves);
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel_lat<true>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel_lat<false>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
     } else {
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
+        if (table) {
+            if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+            else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        } else {
+            if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+            else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
+        }
     }
     HIP_TRY(hipGetLastError());
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
@@ -722,6 +740,13 @@ void dm_destroy(dm_ctx* ctx) {
     for (auto& cm : ctx->comms) (void)ncclCommDestroy(cm);
     for (auto& d : ctx->devs) destroy_device(d);
     delete ctx;
+}
+
+int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
+    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_LATENCY) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->leaf_mode = mode;
+    return DM_OK;
 }
 
 int dm_set_timing(dm_ctx* ctx, int enable) {

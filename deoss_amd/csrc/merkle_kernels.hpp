@@ -209,6 +209,125 @@ __global__ __launch_bounds__(kBlock) void leaf_kernel(LeafArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1L: leaf SHA-256 for few, long leaves (latency regime).  A leaf's compressions form one serial
+// chain, and a wave issues at most one instruction every ~4-6 cycles, so with < ~100 k leaves the
+// root time is (instructions per block on the chain's wave) x (blocks per leaf).  K1L takes the
+// message schedule off that wave: per 64 leaves, wave 0 ("producer") loads the blocks and writes
+// K[t]+W[t] for all 64 rounds into an LDS ring; wave 1 ("consumer") only runs the rounds, reading
+// 4 K+W words per ds_read_b128.  The consumer issues ~64 x 14 + 16 instructions per block instead
+// of ~1,418.  Ring layout [slot][group of 4 rounds][lane] x 16 B: a wave's ds_read_b128 touches 64
+// consecutive 16-byte slots (conflict-free).  Uniform-chunk, single-shot mode only.
+constexpr int kLatLeaves = 64;      // leaves per workgroup (one consumer wave)
+constexpr int kLatThreads = 128;    // producer wave + consumer wave
+constexpr int kLatRing = 2;         // ring slots (producer runs one block ahead)
+constexpr int kLatFuseMax = 6;      // 64 leaves -> 1 node
+
+__device__ __forceinline__ void rounds_from_kw(uint32_t (&st)[8], const uint4 (*kw)[kLatLeaves], uint32_t lane) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    // K+W for 8 rounds in registers, the next 8 rounds' reads in flight (LDS latency hidden)
+    uint4 x = kw[0][lane], y = kw[1][lane];
+#pragma unroll
+    for (int q = 0; q < 16; q += 2) {
+        uint4 nx = x, ny = y;
+        if (q + 2 < 16) {
+            nx = kw[q + 2][lane];
+            ny = kw[q + 3][lane];
+        }
+        DM_SHA_ROUND(a, b, c, d, e, f, g, h, x.x);
+        DM_SHA_ROUND(h, a, b, c, d, e, f, g, x.y);
+        DM_SHA_ROUND(g, h, a, b, c, d, e, f, x.z);
+        DM_SHA_ROUND(f, g, h, a, b, c, d, e, x.w);
+        DM_SHA_ROUND(e, f, g, h, a, b, c, d, y.x);
+        DM_SHA_ROUND(d, e, f, g, h, a, b, c, y.y);
+        DM_SHA_ROUND(c, d, e, f, g, h, a, b, y.z);
+        DM_SHA_ROUND(b, c, d, e, f, g, h, a, y.w);
+        x = nx;
+        y = ny;
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// Message schedule of one block, written as K[t]+W[t] groups of 4 into one ring slot.
+__device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 (*kw)[kLatLeaves], uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int t = 4 * q + j;
+            uint32_t wt;
+            if (t < 16) {
+                wt = w[t];
+            } else {
+                wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                w[t & 15] = wt;
+            }
+            v[j] = kSha256K[t] + wt;
+        }
+        kw[q][lane] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
+    __shared__ uint4 ring[kLatRing][16][kLatLeaves];
+    __shared__ uint32_t lds_a[kLatLeaves][8];
+    __shared__ uint32_t lds_b[kLatLeaves / 2][8];
+    const uint32_t lane = threadIdx.x & (kLatLeaves - 1);
+    // wave-uniform role (readfirstlane makes the branch scalar, so the barriers below pair up)
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < kLatLeaves;
+    const uint64_t first = (uint64_t)blockIdx.x * kLatLeaves;
+    const uint64_t i = first + lane;
+    const bool active = i < a.nleaves;
+    const uint64_t len = active ? ((i + 1 == a.nleaves) ? a.last_len : a.leaf_len) : 0;
+    const uint64_t nb = len / 64;
+    // trip count shared by both waves: only the global last leaf may be shorter
+    const uint64_t NB = (first + 1 < a.nleaves) ? a.leaf_len / 64 : a.last_len / 64;
+    const uint8_t* p = a.base + (active ? i : 0) * a.pitch;
+    uint32_t st[8];
+    if (producer) {
+        Blk cur;
+        if (nb > 0) cur = load_block<ALIGNED>(p);
+        for (uint64_t b = 0; b < NB; b++) {
+            if (b < nb) {
+                uint32_t w[16];
+                block_words(cur, w);
+                if (b + 1 < nb) cur = load_block<ALIGNED>(p + 64 * (b + 1));
+                schedule_to_lds(w, ring[b % kLatRing], lane);
+            }
+            __syncthreads();   // slot b full  /  slot b-1 free
+        }
+        __syncthreads();       // pairs with the consumer's final-iteration barrier
+    } else {
+        init_state(st);
+        __syncthreads();       // wait for slot 0
+        for (uint64_t b = 0; b < NB; b++) {
+            if (b < nb) rounds_from_kw(st, ring[b % kLatRing], lane);
+            __syncthreads();   // slot b consumed; slot b+1 full
+        }
+        if (active) {
+            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(len - 64 * nb), len);
+            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+#pragma unroll
+            for (int k = 0; k < 8; k++) lds_a[lane][k] = st[k];
+        }
+    }
+    if (a.fuse_levels == 0) return;
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((a.nleaves - first) < kLatLeaves ? (a.nleaves - first) : kLatLeaves);
+    uint32_t (*res)[8];
+    const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
+    if (threadIdx.x < out_cnt) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = res[threadIdx.x][k];
+        const uint64_t o = (uint64_t)blockIdx.x * (kLatLeaves >> a.fuse_levels) + threadIdx.x;
+        store_digest(a.level_out + 32 * o, v);
+    }
+}
+
 // K2: tree reduce, `levels` (1..9) levels over tiles of 512 input nodes; the first level reads
 // global memory directly, the rest run in LDS.  Output: ceil(m / 2^levels) nodes.
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const uint8_t* in, uint64_t m, uint32_t levels,

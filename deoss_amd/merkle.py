@@ -155,6 +155,13 @@ class MerkleContext:
         self._check(self._L.dm_fill_synthetic_async(self._h, ctypes.c_void_p(dev_ptr), off, nbytes, seed,
                                                     ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
 
+    # -- tuning --------------------------------------------------------------------------------
+    LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2}
+
+    def set_leaf_kernel(self, mode: str) -> None:
+        """'auto' | 'wide' (one lane per leaf) | 'latency' (producer/consumer waves)."""
+        self._check(self._L.dm_set_leaf_kernel(self._h, self.LEAF_KERNELS[mode]), "dm_set_leaf_kernel")
+
     # -- measurement ----------------------------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         self._check(self._L.dm_set_timing(self._h, int(enable)), "dm_set_timing")

@@ -107,6 +107,14 @@ int dm_root_batch_device_async(dm_ctx *ctx, const void *const *dev_objs, const u
 int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbytes, uint64_t seed,
                             void *stream);
 
+/* ---- tuning ------------------------------------------------------------------------------ */
+
+/* Leaf-kernel selection for uniform-chunk objects (results are identical in every mode):
+ * DM_LEAF_AUTO picks by leaf count; DM_LEAF_WIDE = one lane per leaf (K1, throughput regime);
+ * DM_LEAF_LATENCY = producer/consumer waves per 64 leaves (K1L, few long leaves). */
+enum { DM_LEAF_AUTO = 0, DM_LEAF_WIDE = 1, DM_LEAF_LATENCY = 2 };
+int dm_set_leaf_kernel(dm_ctx *ctx, int mode);
+
 /* ---- measurement ------------------------------------------------------------------------- */
 
 /* Enable (and reset) HIP-event timing: every later call that launches the leaf kernel (K1)

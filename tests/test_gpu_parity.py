@@ -99,7 +99,15 @@ def test_golden_chunks(ctx, golden):
         assert [leaves[32 * i:32 * i + 32].hex() for i in range(len(case["leaves"]))] == case["leaves"], case["name"]
 
 
-def test_golden_buffers_all_paths(ctx, golden):
+@pytest.fixture(params=["wide", "latency"])
+def leaf_mode(request, ctx):
+    """Run a test under each leaf kernel (K1 one-lane-per-leaf, K1L producer/consumer)."""
+    ctx.set_leaf_kernel(request.param)
+    yield request.param
+    ctx.set_leaf_kernel("auto")
+
+
+def test_golden_buffers_all_paths(ctx, golden, leaf_mode):
     for case in golden:
         if case["kind"] != "buffer":
             continue
@@ -139,18 +147,20 @@ def test_golden_batch(ctx, golden):
 
 
 # ---------------------------------------------------------------- edge cases
-def test_leaf_counts_sweep(ctx, oracle_lib):
+def test_leaf_counts_sweep(ctx, oracle_lib, leaf_mode):
     """Every n in 1..600 (odd-node duplication at each level, fused K1 tiles + K2 tiles)."""
-    base = splitmix64_bytes(600 * 64, 11)
+    chunk = 192   # 3 blocks + padding block: several K1L ring rounds per leaf
+    base = splitmix64_bytes(600 * chunk, 11)
     t, ptr = dev_bytes(base)
     for n in list(range(1, 300)) + [311, 383, 384, 385, 511, 512, 513, 599, 600]:
-        length = n * 64 - (n % 7)      # ragged last chunk for most n
-        _, want = oracle_lib.root_buffer(base[:length], 64)
-        got, _ = root_dev(ctx, ptr, length, 64)
+        length = n * chunk - (n % 7) * 29      # ragged last chunk for most n
+        lw, want = oracle_lib.root_buffer(base[:length], chunk)
+        got, lv = root_dev(ctx, ptr, length, chunk, want_leaves=True)
         assert got == want, n
+        assert lv[:len(lw)] == lw, n
 
 
-def test_padding_boundaries_device(ctx, oracle_lib):
+def test_padding_boundaries_device(ctx, oracle_lib, leaf_mode):
     for chunk in (1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 128, 1000, 4096):
         for length in (1, chunk, chunk + 1, 3 * chunk - 1, 5 * chunk):
             buf = splitmix64_bytes(length, chunk * 1000 + length)
@@ -161,7 +171,7 @@ def test_padding_boundaries_device(ctx, oracle_lib):
             assert lv[:len(lw)] == lw
 
 
-def test_many_leaves_multi_stage(ctx, oracle_lib):
+def test_many_leaves_multi_stage(ctx, oracle_lib, leaf_mode):
     """> 2^17 leaves: K1 fused 8 levels + two K2 launches (9 + rest)."""
     torch = _torch()
     length, chunk = (1 << 18) * 64 + 17, 64
@@ -189,7 +199,7 @@ def test_empty_and_invalid(ctx):
 
 # ---------------------------------------------------------------- sharding (subtree + finish)
 @pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world):
+def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world, leaf_mode):
     """The multi-GPU decomposition (deoss_amd.sharding) on one device: per-rank subtree to k
     levels on each rank's byte range, concatenate, finish == the single-object root."""
     torch = _torch()
