@@ -69,9 +69,14 @@ def main() -> None:
     ap.add_argument("--no-sweep", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
     ap.add_argument("--sweep-modes", action="store_true", help="sweep both leaf kernels (wide, latency)")
     ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency"])
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo = CPU exchange (rehearsal on one GPU)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (with --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -84,10 +89,15 @@ def main() -> None:
     local_rank = env_int("LOCAL_RANK", 0)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = 0 if args.same_device else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    gloo = args.dist_backend == "gloo"
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        if gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
     per_gpu = int(args.object_gib * (1 << 30))
     chunk = args.chunk
@@ -95,7 +105,7 @@ def main() -> None:
     plan = plan_shards(total, chunk, world)
     b0, b1 = plan.byte_range(rank)
     local_len = b1 - b0
-    ctx = MerkleContext(devices=[local_rank])
+    ctx = MerkleContext(devices=[dev_index])
     ctx.set_leaf_kernel(args.leaf_kernel)
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
@@ -116,11 +126,16 @@ def main() -> None:
         if world == 1:
             ctx.root_device_async(buf.data_ptr(), local_len, chunk, root_dev.data_ptr(), 0, sptr)
         else:
-            sharded_root(plan, rank, subtree, finish, torch, dist, device)
+            sharded_root(plan, rank, subtree, finish, torch, dist, device,
+                         comm_device="cpu" if gloo else None)
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local_rank])
+            if gloo:
+                torch.cuda.synchronize()
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[dev_index])
         torch.cuda.synchronize()
 
     for _ in range(args.warmup):
@@ -137,7 +152,7 @@ def main() -> None:
     ctx.set_timing(False)
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     root_hex = bytes(root_dev.cpu().numpy()).hex() if rank == 0 else None
@@ -192,10 +207,21 @@ def main() -> None:
 
     if world == 1 and rank == 0:
         extras(args, ctx, torch, buf, local_len, chunk, root_hex, out, sptr)
+    if world > 1 and rank == 0 and not args.no_verify:
+        # untimed: the sharded root must equal the single-GPU root of the whole object
+        del buf
+        full = torch.empty(total + 64, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic_async(full.data_ptr(), 0, (total + 7) // 8 * 8, SEED, sptr)
+        one = torch.zeros(32, dtype=torch.uint8, device=device)
+        ctx.root_device_async(full.data_ptr(), total, chunk, one.data_ptr(), 0, sptr)
+        torch.cuda.synchronize()
+        single = bytes(one.cpu().numpy()).hex()
+        out["parity"] = {"sharded_root": root_hex, "single_gpu_root": single, "bit_exact": single == root_hex}
+        del full
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.barrier(device_ids=[local_rank])
+        barrier()
         dist.destroy_process_group()
 
 

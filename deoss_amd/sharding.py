@@ -67,24 +67,26 @@ def plan_shards(length: int, chunk: int, world: int) -> ShardPlan:
 
 def sharded_root(plan: ShardPlan, rank: int, local_subtree: Callable[[int], "object"],
                  finish: Callable[["object", int, bool], "object"], torch_mod, dist_mod,
-                 device, group=None):
+                 device, group=None, comm_device=None):
     """Run one sharded root computation.
 
     local_subtree(k) -> uint8 tensor of this rank's level-k nodes (node_count(rank) * 32 bytes)
     finish(nodes, n, min_one_level) -> 32-byte root tensor (rank 0 only)
     Returns the root tensor on rank 0 and None elsewhere.  The only data exchange is one
     all_gather_into_tensor of fixed-size slots (max_nodes * 32 bytes per rank).
+    comm_device: where the exchange buffers live (default: device; "cpu" for a gloo group).
     """
+    comm = device if comm_device is None else comm_device
     slot = plan.max_nodes * 32
     mine = local_subtree(plan.k)
     cnt = plan.node_count(rank)
-    if cnt * 32 == slot:
-        send = mine
+    if cnt * 32 == slot and str(comm) == str(device):
+        send = mine[:slot]
     else:
-        send = torch_mod.zeros(slot, dtype=torch_mod.uint8, device=device)
+        send = torch_mod.zeros(slot, dtype=torch_mod.uint8, device=comm)
         if cnt:
-            send[:cnt * 32] = mine[:cnt * 32]
-    gathered = torch_mod.empty(plan.world * slot, dtype=torch_mod.uint8, device=device)
+            send[:cnt * 32] = mine[:cnt * 32].to(comm)
+    gathered = torch_mod.empty(plan.world * slot, dtype=torch_mod.uint8, device=comm)
     dist_mod.all_gather_into_tensor(gathered, send, group=group)
     if rank != 0:
         return None
@@ -94,4 +96,6 @@ def sharded_root(plan: ShardPlan, rank: int, local_subtree: Callable[[int], "obj
         if c:
             parts.append(gathered[r * slot:r * slot + c * 32])
     nodes = parts[0] if len(parts) == 1 else torch_mod.cat(parts)
+    if str(comm) != str(device):
+        nodes = nodes.to(device)
     return finish(nodes, plan.n_blocks, plan.k == 0)
