@@ -72,7 +72,7 @@ def main() -> None:
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
     ap.add_argument("--sweep-modes", action="store_true", help="sweep both leaf kernels (wide, latency)")
-    ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency"])
+    ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = CPU exchange (rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
@@ -262,7 +262,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     if not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
-        modes = ["wide", "latency"] if args.sweep_modes else ["auto"]
+        modes = ["wide", "latency", "pair"] if args.sweep_modes else ["auto"]
         for c, mode in [(int(x), m) for x in args.sweep_chunks.split(",") for m in modes]:
             ctx.set_leaf_kernel(mode)
             reps = 3 if c < (8 << 20) else 2

@@ -228,19 +228,21 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // (levels < 0: to the root, >= 1 level).  Nodes go to dst; *nout gets their count.
 // Leaf-kernel choice for a uniform-chunk object of n leaves: the producer/consumer latency
 // kernel (K1L) while the leaves cannot fill the chip, the one-lane-per-leaf kernel (K1) after.
-bool use_latency_kernel(const dm_ctx* c, uint64_t n, bool table) {
-    if (table) return false;
-    if (c->leaf_mode == DM_LEAF_WIDE) return false;
-    if (c->leaf_mode == DM_LEAF_LATENCY) return true;
-    return n <= kLatencyLeafMax;
+// Returns DM_LEAF_WIDE, DM_LEAF_LATENCY or DM_LEAF_PAIR.
+int pick_leaf_kernel(const dm_ctx* c, uint64_t n, bool table) {
+    if (table) return DM_LEAF_WIDE;
+    if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
+    return n <= kLatencyLeafMax ? DM_LEAF_PAIR : DM_LEAF_WIDE;
 }
 
 int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool aligned, int levels,
              uint8_t* dst, uint64_t* nout, uint8_t* leaf_dig) {
     const uint64_t n = la.nleaves;
-    const bool lat = use_latency_kernel(c, n, table);
+    const int kind = pick_leaf_kernel(c, n, table);
     const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
-    const uint32_t L1 = std::min<uint32_t>(lat ? dm::kLatFuseMax : dm::kLeafFuseMax, D);
+    const uint32_t fuse_max = kind == DM_LEAF_PAIR ? dm::kPairFuseMax
+                              : kind == DM_LEAF_LATENCY ? dm::kLatFuseMax : dm::kLeafFuseMax;
+    const uint32_t L1 = std::min<uint32_t>(fuse_max, D);
     const uint64_t m1 = ceil_shift(n, L1);
     la.byte_off = 0;
     la.byte_end = ~0ull;
@@ -260,7 +262,11 @@ int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool
     }
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    if (lat) {
+    if (kind == DM_LEAF_PAIR) {
+        const uint32_t grid = (uint32_t)ceil_div(n, dm::kPairLeaves);
+        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel_pair<true>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
+        else hipLaunchKernelGGL((dm::leaf_kernel_pair<false>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
+    } else if (kind == DM_LEAF_LATENCY) {
         const uint32_t grid = (uint32_t)ceil_div(n, dm::kLatLeaves);
         if (aligned) hipLaunchKernelGGL((dm::leaf_kernel_lat<true>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
         else hipLaunchKernelGGL((dm::leaf_kernel_lat<false>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
@@ -743,7 +749,7 @@ void dm_destroy(dm_ctx* ctx) {
 }
 
 int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
-    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_LATENCY) return DM_ERR_INVALID;
+    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_PAIR) return DM_ERR_INVALID;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->leaf_mode = mode;
     return DM_OK;

@@ -328,6 +328,146 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1P: K1L with the rounds packed on lane pairs.  Consumer lanes 2c (A) and 2c+1 (B) run leaf c:
+// A holds (e,f,g,h), B holds (a,b,c,d) in the same four registers X4..X7, and every instruction
+// of a round does both halves with per-lane operands:
+//   S = x3(rotr(X4,s1), rotr(X4,s2), rotr(X4,s3))  A: Sigma1(e)  B: Sigma0(a)   (per-lane shifts)
+//   x = X4 ^ (X5 | M)                               A: ~e        B: a ^ b       (M = ~0 on A)
+//   F = (x & X6) | (~x & X5)                        A: Ch(e,f,g) B: Maj(a,b,c)
+//   T = S + F + (X7 & M) + KW                       A: T1        B: T2          (KW = 0 on B)
+//   Y = B ? X7 : T                                  A: T1        B: d
+//   X4' = T + Y[lane ^ 1]  (one DPP add)            A: d + T1    B: T1 + T2
+// i.e. 11 instructions per round instead of 14; the message schedule stays on the producer.
+constexpr int kPairLeaves = 32;     // leaves per workgroup (two consumer lanes per leaf)
+constexpr int kPairFuseMax = 5;     // 32 leaves -> 1 node
+
+__device__ __forceinline__ uint32_t dpp_swap_pairs(uint32_t v) {
+    // quad_perm [1,0,3,2]: lane i reads lane i^1
+    // old = 0 with bound_ctrl: the identity of the consuming add, so hipcc's DPP-combine pass can
+    // fold this move into v_add_u32_dpp
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);
+}
+
+#define DM_PAIR_ROUND(X4, X5, X6, X7, kw)                                              \
+    do {                                                                               \
+        const uint32_t s_ = xor3(__builtin_amdgcn_alignbit(X4, X4, sh1),               \
+                                 __builtin_amdgcn_alignbit(X4, X4, sh2),               \
+                                 __builtin_amdgcn_alignbit(X4, X4, sh3));              \
+        const uint32_t x_ = __builtin_amdgcn_bitop3_b32(X4, X5, msk, 0x1e);            \
+        const uint32_t f_ = __builtin_amdgcn_bitop3_b32(x_, X6, X5, 0xca);             \
+        const uint32_t t_ = s_ + f_ + ((X7 & msk) + (kw));                             \
+        const uint32_t y_ = lane_b ? X7 : t_;                                          \
+        X7 = t_ + dpp_swap_pairs(y_);                                                  \
+    } while (0)
+
+__device__ __forceinline__ void pair_rounds_from_kw(uint32_t (&x)[4], const uint4 (*kw)[kLatLeaves], uint32_t lane,
+                                                    uint32_t sh1, uint32_t sh2, uint32_t sh3, uint32_t msk,
+                                                    bool lane_b) {
+    uint32_t x4 = x[0], x5 = x[1], x6 = x[2], x7 = x[3];
+    uint4 q = kw[0][lane];
+#pragma unroll
+    for (int g = 0; g < 16; g++) {
+        uint4 nq = q;
+        if (g + 1 < 16) nq = kw[g + 1][lane];
+        // register roles rotate: after a round, the new value X4' lands in the old X7 register
+        DM_PAIR_ROUND(x4, x5, x6, x7, q.x);   // new x4 in x7
+        DM_PAIR_ROUND(x7, x4, x5, x6, q.y);   // new in x6
+        DM_PAIR_ROUND(x6, x7, x4, x5, q.z);   // new in x5
+        DM_PAIR_ROUND(x5, x6, x7, x4, q.w);   // new in x4
+        q = nq;
+    }
+    x[0] += x4; x[1] += x5; x[2] += x6; x[3] += x7;
+}
+
+template <bool ALIGNED>
+__global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
+    __shared__ uint4 ring[kLatRing][16][kLatLeaves];
+    __shared__ uint32_t lds_a[kPairLeaves][8];
+    __shared__ uint32_t lds_b[kPairLeaves / 2][8];
+    const uint32_t lane = threadIdx.x & (kLatLeaves - 1);
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < kLatLeaves;
+    const bool lane_b = (lane & 1) != 0;
+    const uint32_t c = lane >> 1;                           // leaf within the workgroup
+    const uint64_t first = (uint64_t)blockIdx.x * kPairLeaves;
+    const uint64_t i = first + c;
+    const bool active = i < a.nleaves;
+    const uint64_t len = active ? ((i + 1 == a.nleaves) ? a.last_len : a.leaf_len) : 0;
+    const uint64_t nb = len / 64;
+    const uint64_t NB = (first + 1 < a.nleaves) ? a.leaf_len / 64 : a.last_len / 64;
+    const uint8_t* p = a.base + (active ? i : 0) * a.pitch;
+    if (producer) {
+        // even lanes compute leaf c's K+W; odd lanes publish zeros (the B half adds no K+W)
+        Blk cur;
+        if (nb > 0 && !lane_b) cur = load_block<ALIGNED>(p);
+        for (uint64_t b = 0; b < NB; b++) {
+            if (b < nb) {
+                uint32_t w[16];
+                block_words(cur, w);
+                if (b + 1 < nb && !lane_b) cur = load_block<ALIGNED>(p + 64 * (b + 1));
+                uint4 (*kw)[kLatLeaves] = ring[b % kLatRing];
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    uint32_t v[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int t = 4 * q + j;
+                        uint32_t wt;
+                        if (t < 16) {
+                            wt = w[t];
+                        } else {
+                            wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                            w[t & 15] = wt;
+                        }
+                        v[j] = lane_b ? 0u : kSha256K[t] + wt;
+                    }
+                    kw[q][lane] = make_uint4(v[0], v[1], v[2], v[3]);
+                }
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+    } else {
+        // per-lane constants of the packed round
+        const uint32_t sh1 = lane_b ? 2 : 6, sh2 = lane_b ? 13 : 11, sh3 = lane_b ? 22 : 25;
+        const uint32_t msk = lane_b ? 0u : ~0u;
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = lane_b ? kIV[k] : kIV[4 + k];
+        __syncthreads();
+        for (uint64_t b = 0; b < NB; b++) {
+            if (b < nb) pair_rounds_from_kw(x, ring[b % kLatRing], lane, sh1, sh2, sh3, msk, lane_b);
+            __syncthreads();
+        }
+        // reassemble the full state on lane A: (a,b,c,d) from lane B, (e,f,g,h) own
+        uint32_t st[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t other = dpp_swap_pairs(x[k]);
+            st[k] = lane_b ? x[k] : other;
+            st[4 + k] = lane_b ? other : x[k];
+        }
+        if (active && !lane_b) {
+            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(len - 64 * nb), len);
+            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+#pragma unroll
+            for (int k = 0; k < 8; k++) lds_a[c][k] = st[k];
+        }
+    }
+    if (a.fuse_levels == 0) return;
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((a.nleaves - first) < kPairLeaves ? (a.nleaves - first) : kPairLeaves);
+    uint32_t (*res)[8];
+    const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
+    if (threadIdx.x < out_cnt) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = res[threadIdx.x][k];
+        const uint64_t o = (uint64_t)blockIdx.x * (kPairLeaves >> a.fuse_levels) + threadIdx.x;
+        store_digest(a.level_out + 32 * o, v);
+    }
+}
+
 // K2: tree reduce, `levels` (1..9) levels over tiles of 512 input nodes; the first level reads
 // global memory directly, the rest run in LDS.  Output: ceil(m / 2^levels) nodes.
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const uint8_t* in, uint64_t m, uint32_t levels,

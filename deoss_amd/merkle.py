@@ -156,10 +156,11 @@ class MerkleContext:
                                                     ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
 
     # -- tuning --------------------------------------------------------------------------------
-    LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2}
+    LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2, "pair": 3}
 
     def set_leaf_kernel(self, mode: str) -> None:
-        """'auto' | 'wide' (one lane per leaf) | 'latency' (producer/consumer waves)."""
+        """'auto' | 'wide' (one lane per leaf) | 'latency' (producer/consumer waves) |
+        'pair' (producer/consumer with rounds packed on lane pairs)."""
         self._check(self._L.dm_set_leaf_kernel(self._h, self.LEAF_KERNELS[mode]), "dm_set_leaf_kernel")
 
     # -- measurement ----------------------------------------------------------------------------

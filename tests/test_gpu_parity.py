@@ -99,7 +99,7 @@ def test_golden_chunks(ctx, golden):
         assert [leaves[32 * i:32 * i + 32].hex() for i in range(len(case["leaves"]))] == case["leaves"], case["name"]
 
 
-@pytest.fixture(params=["wide", "latency"])
+@pytest.fixture(params=["wide", "latency", "pair"])
 def leaf_mode(request, ctx):
     """Run a test under each leaf kernel (K1 one-lane-per-leaf, K1L producer/consumer)."""
     ctx.set_leaf_kernel(request.param)
