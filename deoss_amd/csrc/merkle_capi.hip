@@ -31,7 +31,6 @@ namespace {
 constexpr uint64_t kAlign = 256;                    // leaf start alignment when packing chunks
 constexpr uint64_t kStageBytes = 64ull << 20;       // pinned staging slot
 constexpr uint64_t kStripeBudget = 256ull << 20;    // bytes per H2D stripe / batch (e2e path)
-constexpr uint64_t kLatencyLeafMax = 32768;         // auto mode: K1L up to this many leaves
 
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
@@ -91,6 +90,7 @@ struct PinnedBuf {
 
 struct Dev {
     int id = 0;
+    int cus = 256;                      // compute units (leaf-kernel choice)
     hipStream_t stream = nullptr;       // compute stream
     hipStream_t copy = nullptr;         // H2D stream
     DevBuf data, nodes_a, nodes_b, leaves, tab_addr, tab_len, tab_first, tab_ids, root, gather;
@@ -229,16 +229,21 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // Leaf-kernel choice for a uniform-chunk object of n leaves: the producer/consumer latency
 // kernel (K1L) while the leaves cannot fill the chip, the one-lane-per-leaf kernel (K1) after.
 // Returns DM_LEAF_WIDE, DM_LEAF_LATENCY or DM_LEAF_PAIR.
-int pick_leaf_kernel(const dm_ctx* c, uint64_t n, bool table) {
+// Measured (profiles/r01_bench_modes.log, r01_crossover.log): the latency kernels win while
+// every workgroup gets a CU of its own (one consumer wave per SIMD); past that, one lane per
+// leaf with >= 2 waves per SIMD wins.
+int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n, bool table) {
     if (table) return DM_LEAF_WIDE;
     if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
-    return n <= kLatencyLeafMax ? DM_LEAF_PAIR : DM_LEAF_WIDE;
+    if (ceil_div(n, dm::kPairLeaves) <= (uint64_t)d.cus) return DM_LEAF_PAIR;
+    if (ceil_div(n, dm::kLatLeaves) <= (uint64_t)d.cus) return DM_LEAF_LATENCY;
+    return DM_LEAF_WIDE;
 }
 
 int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool aligned, int levels,
              uint8_t* dst, uint64_t* nout, uint8_t* leaf_dig) {
     const uint64_t n = la.nleaves;
-    const int kind = pick_leaf_kernel(c, n, table);
+    const int kind = pick_leaf_kernel(c, d, n, table);
     const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
     const uint32_t fuse_max = kind == DM_LEAF_PAIR ? dm::kPairFuseMax
                               : kind == DM_LEAF_LATENCY ? dm::kLatFuseMax : dm::kLeafFuseMax;
@@ -543,6 +548,7 @@ int root_device_impl(dm_ctx* c, Dev& d, hipStream_t s, const void* dev, uint64_t
 
 int init_device(dm_ctx* c, Dev& d) {
     HIP_TRY(hipSetDevice(d.id));
+    HIP_TRY(hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
