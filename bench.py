@@ -44,19 +44,24 @@ def blocks_for(length: int, chunk: int) -> int:
     return leaf_blocks + 2 * nodes
 
 
-def load_traffic(n_leaves: int):
-    """PMC HBM bytes per K1 launch for this launch shape, from the committed rocprofv3 passes
-    (profiles/k1_traffic.json, made by tools/pmc_traffic.py from the same bench command)."""
+LEAF_GRID = {"wide": (256, 256), "latency": (64, 128), "pair": (32, 128)}   # leaves, threads per WG
+
+
+def load_traffic(kind: str, n_leaves: int):
+    """PMC HBM bytes per leaf-kernel launch of this kernel and launch shape, from the committed
+    rocprofv3 passes (profiles/k1_traffic.json, made by tools/pmc_traffic.py from the same
+    bench command)."""
     path = os.path.join(ROOT, "profiles", "k1_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
-    grid = str((n_leaves + 255) // 256 * 256)
-    e = d.get("by_grid_threads", {}).get(grid)
+    per_wg, threads = LEAF_GRID[kind]
+    key = f"{kind}:{(n_leaves + per_wg - 1) // per_wg * threads}"
+    e = d.get("by_kernel_grid", {}).get(key)
     if not e:
         return None, None
-    return e["hbm_bytes_per_launch"], "profiles/k1_traffic.json <- " + d.get("source", "")
+    return e["hbm_bytes_per_launch"], f"profiles/k1_traffic.json[{key}] <- " + d.get("source", "")
 
 
 def main() -> None:
@@ -162,9 +167,14 @@ def main() -> None:
     k1_bytes = local_len + 32 * ((local_len + chunk - 1) // chunk)   # read N once + 32 B per leaf
     achieved_gbs = k1_bytes / (k1_avg_ms * 1e-3) / 1e9 if k1_avg_ms > 0 else 0.0
     blocks = blocks_for(local_len, chunk)
-    from deoss_amd.isa import valu_per_block
-    vpb, spb = valu_per_block()
-    traffic, traffic_src = load_traffic((local_len + chunk - 1) // chunk)
+    from deoss_amd.isa import kernel_counts
+    n_local = (local_len + chunk - 1) // chunk
+    kind = ctx.leaf_kernel_for(n_local)
+    vpb, spb = kernel_counts(kind)
+    traffic, traffic_src = load_traffic(kind, n_local)
+    kernel_name = {"wide": "leaf_kernel (K1, one lane per leaf)",
+                   "latency": "leaf_kernel_lat (K1L, producer/consumer waves)",
+                   "pair": "leaf_kernel_pair (K1P, producer/consumer, rounds on lane pairs)"}[kind]
 
     out = {
         "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling",
@@ -187,20 +197,23 @@ def main() -> None:
                            f"RCCL all-gather of subtree roots" if world > 1 else "single GPU",
         },
         "roofline": {
-            "bound": "hbm", "kernel": "leaf_kernel (K1)",
+            "bound": "hbm", "kernel": kernel_name,
             "achieved": round(achieved_gbs, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
             "traffic": traffic, "traffic_source": traffic_src,
             "k1_avg_ms": round(k1_avg_ms, 4), "k1_launches": ncalls,
             "algorithmic_bytes_per_launch": k1_bytes,
             "valu": {
-                "ops_per_block": vpb, "slots_per_block": spb, "blocks_per_step": blocks,
+                "critical_wave_valu_per_block": vpb, "lane_slots_per_leaf_block": spb, "blocks_per_step": blocks,
                 "achieved_slots_per_s": (blocks * spb / (k1_avg_ms * 1e-3)) if (spb and k1_avg_ms) else None,
                 "peak_slots_per_s": VALU_SLOT_PEAK,
                 "frac": round(blocks * spb / (k1_avg_ms * 1e-3) / VALU_SLOT_PEAK, 6) if (spb and k1_avg_ms) else None,
                 "note": "SHA-256 is bound by integer VALU issue, not HBM; v_alignbit/v_add3 cost 2 slots "
                         "(measured, tools/valu_peak.hip); see DESIGN.md",
             },
+            "regime": ("latency-bound: each leaf is one serial SHA-256 chain; rate = leaves x per-leaf rate"
+                       if kind != "wide" else "throughput (VALU issue)"),
+            "per_leaf_MBps": round(local_len / n_local / (k1_avg_ms * 1e-3) / 1e6, 3) if k1_avg_ms else None,
         },
         "root": root_hex,
     }

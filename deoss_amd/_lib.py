@@ -28,7 +28,8 @@ EXPORTS = (
     "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count",
     "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
     "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
-    "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_set_leaf_kernel", "dm_set_timing",
+    "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_set_leaf_kernel", "dm_leaf_kernel_for",
+    "dm_set_timing",
     "dm_timing_summary",
 )
 
@@ -63,6 +64,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_root_batch_device_async": ([vp, pvp, pu64, u64, u64, vp, vp], i32),
         "dm_fill_synthetic_async": ([vp, vp, u64, u64, u64, vp], i32),
         "dm_set_leaf_kernel": ([vp, i32], i32),
+        "dm_leaf_kernel_for": ([vp, u64], i32),
         "dm_set_timing": ([vp, i32], i32),
         "dm_timing_summary": ([vp, pu64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double)], i32),

@@ -761,6 +761,12 @@ int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
     return DM_OK;
 }
 
+int dm_leaf_kernel_for(dm_ctx* ctx, uint64_t nleaves) {
+    if (!ctx) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return pick_leaf_kernel(ctx, ctx->devs[0], nleaves, false);
+}
+
 int dm_set_timing(dm_ctx* ctx, int enable) {
     if (!ctx) return DM_ERR_INVALID;
     std::lock_guard<std::mutex> lk(ctx->mu);

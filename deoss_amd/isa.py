@@ -1,9 +1,16 @@
-"""Static instruction counts of the compiled K1 loop, for the VALU roofline.
+"""Static instruction counts of the compiled leaf-kernel loops, for the VALU roofline.
 
-``python -m deoss_amd.isa`` recompiles merkle_capi.hip with ``-save-temps``, finds the block
-loop of ``leaf_kernel<false,true>`` (uniform chunks, 16-B aligned: the bench path) and counts its
-VALU instructions per 64-byte block; the result is written to ``isa_counts.json`` next to this
-file (it travels with the built library).
+``python -m deoss_amd.isa`` recompiles merkle_capi.hip with ``-save-temps`` and, for each
+leaf kernel (16-B aligned variants: the bench path), finds its per-block loop in the gfx950
+assembly and counts the instructions of one 64-byte block:
+
+* ``wide`` (K1, one lane per leaf): the loop streaming 4 x global_load_dwordx4 per block;
+* ``latency`` (K1L) and ``pair`` (K1P): the consumer loop (16 ds_read_b128 of K+W per block)
+  and the producer loop (16 ds_write_b128 per block).
+
+``lanes_per_leaf`` converts wave-instruction counts into lane-slots per leaf-block: K1 runs one
+lane per leaf, K1L two (producer + consumer lane), K1P four (two of each).  Results go to
+``isa_counts.json`` next to this file (it travels with the built library).
 """
 from __future__ import annotations
 
@@ -14,12 +21,17 @@ import subprocess
 import tempfile
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+COUNTS = os.path.join(HERE, "isa_counts.json")
 # Issue slots per wave64 instruction relative to v_add_u32, measured on MI355X by
 # tools/valu_peak.hip (profiles/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
 # the v_add_u32 / v_bitop3_b32 rate.
 SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0}
-COUNTS = os.path.join(HERE, "isa_counts.json")
-K1_SYMBOL = "_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE"
+KERNELS = {
+    "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", 1),
+    "latency": ("_ZN2dm15leaf_kernel_latILb1EEEvNS_8LeafArgsE", 2),
+    "pair": ("_ZN2dm16leaf_kernel_pairILb1EEEvNS_8LeafArgsE", 4),
+}
+K1_SYMBOL = KERNELS["wide"][0]
 
 
 def _function_body(asm: str, sym: str) -> list:
@@ -39,51 +51,63 @@ def _function_body(asm: str, sym: str) -> list:
     return body
 
 
-def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
-    """Find the hottest loop (largest basic-block chain ending in a backward branch)."""
-    body = _function_body(asm, sym)
-    labels = {}
-    insts = []   # (index, text)
+def _loops(body: list):
+    """Yield the instruction list of every backward-branch loop."""
+    labels, insts = {}, []
     for ln in body:
         s = ln.strip()
-        if not s or s.startswith(";") or s.startswith("."):
-            m = re.match(r"^(\.LBB[0-9_]+):", s)
-            if m:
-                labels[m.group(1)] = len(insts)
-            continue
         m = re.match(r"^(\.LBB[0-9_]+):", s)
         if m:
             labels[m.group(1)] = len(insts)
             continue
+        if not s or s.startswith(";") or s.startswith("."):
+            continue
         insts.append(s.split(";")[0].strip())
-    best = None
     for i, ins in enumerate(insts):
-        m = re.match(r"^s_cbranch_\w+\s+(\.LBB[0-9_]+)", ins) or re.match(r"^s_branch\s+(\.LBB[0-9_]+)", ins)
-        if not m or m.group(1) not in labels:
-            continue
-        tgt = labels[m.group(1)]
-        if tgt > i:
-            continue
-        loop = insts[tgt:i + 1]
-        loads = sum(1 for x in loop if x.startswith("global_load_dwordx4"))
-        if loads < 4:      # the block loop streams 64 B per iteration (4 x dwordx4)
-            continue
-        if best is not None and len(loop) >= best["total"]:
-            continue
-        valu = [x for x in loop if x.startswith("v_")]
-        hist = {}
-        for x in valu:
-            op = x.split()[0]
-            hist[op] = hist.get(op, 0) + 1
-        per = max(1, loads // 4)   # 64-byte blocks per loop iteration
-        slots = sum(SLOT_WEIGHTS.get(x.split()[0], 1.0) for x in valu)
-        best = {"valu": round(len(valu) / per, 1), "valu_slots": round(slots / per, 1), "blocks_per_iteration": per,
-                "valu_per_iteration": len(valu), "salu": sum(1 for x in loop if x.startswith("s_")),
-                "vmem": sum(1 for x in loop if x.startswith(("global_", "buffer_", "flat_"))),
-                "total": len(loop), "valu_histogram": dict(sorted(hist.items(), key=lambda kv: -kv[1]))}
-    if best is None:
-        raise ValueError("no loop found")
+        m = re.match(r"^s_c?branch\w*\s+(\.LBB[0-9_]+)", ins)
+        if m and m.group(1) in labels and labels[m.group(1)] <= i:
+            yield insts[labels[m.group(1)]:i + 1]
+
+
+def _summary(loop: list, per: int) -> dict:
+    valu = [x for x in loop if x.startswith("v_")]
+    hist = {}
+    for x in valu:
+        op = x.split()[0]
+        hist[op] = hist.get(op, 0) + 1
+    slots = sum(SLOT_WEIGHTS.get(x.split()[0], 1.0) for x in valu)
+    return {"valu": round(len(valu) / per, 1), "valu_slots": round(slots / per, 1),
+            "blocks_per_iteration": per, "salu": sum(1 for x in loop if x.startswith("s_")),
+            "lds": sum(1 for x in loop if x.startswith("ds_")),
+            "vmem": sum(1 for x in loop if x.startswith(("global_", "buffer_", "flat_"))),
+            "total": len(loop), "valu_histogram": dict(sorted(hist.items(), key=lambda kv: -kv[1]))}
+
+
+def _smallest(loops, pred):
+    best = None
+    for lp in loops:
+        if pred(lp) and (best is None or len(lp) < len(best)):
+            best = lp
     return best
+
+
+def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
+    """Per-block counts of the wide kernel's streaming loop."""
+    loops = list(_loops(_function_body(asm, sym)))
+    lp = _smallest(loops, lambda l: sum(x.startswith("global_load_dwordx4") for x in l) >= 4)
+    if lp is None:
+        raise ValueError("no block loop found")
+    loads = sum(x.startswith("global_load_dwordx4") for x in lp)
+    return _summary(lp, max(1, loads // 4))
+
+
+def analyse_split(asm: str, sym: str) -> dict:
+    loops = list(_loops(_function_body(asm, sym)))
+    cons = _smallest(loops, lambda l: sum(x.startswith("ds_read_b128") for x in l) >= 16)
+    prod = _smallest(loops, lambda l: sum(x.startswith("ds_write_b128") for x in l) >= 16)
+    if cons is None or prod is None:
+        raise ValueError(f"{sym}: consumer/producer loop not found")
+    return {"consumer": _summary(cons, 1), "producer": _summary(prod, 1)}
 
 
 def generate() -> dict:
@@ -94,22 +118,37 @@ def generate() -> dict:
         subprocess.run(cmd, check=True, cwd=td, capture_output=True)
         asm_files = [f for f in os.listdir(td) if f.endswith(".s") and "gfx950" in f]
         asm = open(os.path.join(td, asm_files[0])).read()
-    res = analyse(asm)
-    res["kernel"] = K1_SYMBOL
-    res["per"] = "one 64-byte block (loop iteration of absorb_blocks)"
+    res = {}
+    for name, (sym, lanes) in KERNELS.items():
+        if name == "wide":
+            d = analyse(asm, sym)
+            d["lane_slots_per_leaf_block"] = d["valu_slots"]
+        else:
+            d = analyse_split(asm, sym)
+            d["lane_slots_per_leaf_block"] = (d["consumer"]["valu_slots"] + d["producer"]["valu_slots"]) * lanes / 2
+            d["consumer_valu_per_block"] = d["consumer"]["valu"]
+        d["kernel"] = sym
+        d["lanes_per_leaf"] = lanes
+        res[name] = d
+    res["per"] = "one 64-byte block of one leaf"
     with open(COUNTS, "w") as f:
         json.dump(res, f, indent=1)
     return res
 
 
-def valu_per_block():
-    """(VALU instructions, full-rate issue slots) per 64-byte block of the K1 loop."""
+def kernel_counts(kind: str = "wide"):
+    """(VALU instructions per block on the leaf's critical wave, lane-slots per leaf-block)."""
     try:
         with open(COUNTS) as f:
-            d = json.load(f)
-            return d["valu"], d["valu_slots"]
+            d = json.load(f)[kind]
     except (OSError, KeyError, ValueError):
         return None, None
+    ops = d["valu"] if kind == "wide" else d["consumer_valu_per_block"]
+    return ops, d["lane_slots_per_leaf_block"]
+
+
+def valu_per_block():
+    return kernel_counts("wide")
 
 
 if __name__ == "__main__":

@@ -163,6 +163,13 @@ class MerkleContext:
         'pair' (producer/consumer with rounds packed on lane pairs)."""
         self._check(self._L.dm_set_leaf_kernel(self._h, self.LEAF_KERNELS[mode]), "dm_set_leaf_kernel")
 
+    def leaf_kernel_for(self, nleaves: int) -> str:
+        """Leaf kernel ('wide' | 'latency' | 'pair') an object of nleaves uniform chunks runs with."""
+        code = self._L.dm_leaf_kernel_for(self._h, nleaves)
+        if code < 0:
+            self._check(code, "dm_leaf_kernel_for")
+        return {v: k for k, v in self.LEAF_KERNELS.items()}[code]
+
     # -- measurement ----------------------------------------------------------------------------
     def set_timing(self, enable: bool) -> None:
         self._check(self._L.dm_set_timing(self._h, int(enable)), "dm_set_timing")

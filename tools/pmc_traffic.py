@@ -19,12 +19,20 @@ import sys
 KERNEL = "leaf_kernel"
 
 
+def kind(name: str) -> str:
+    if "leaf_kernel_pair" in name:
+        return "pair"
+    if "leaf_kernel_lat" in name:
+        return "latency"
+    return "wide"
+
+
 def rows(path):
     out = []
     with open(path) as f:
         for r in csv.DictReader(f):
             if KERNEL in r["Kernel_Name"]:
-                out.append((int(r["Grid_Size"]), float(r["Counter_Value"])))
+                out.append((f'{kind(r["Kernel_Name"])}:{int(r["Grid_Size"])}', float(r["Counter_Value"])))
     return out
 
 
@@ -45,7 +53,7 @@ def main():
                       "write_kib_per_launch": sum(x["write_kib"] for x in lst) / len(lst)}
     res = {"source": f"{os.path.basename(fetch)} + {os.path.basename(write)} (rocprofv3 --pmc, separate passes)",
            "kernel": KERNEL, "correction": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950, 16 B/lane)",
-           "by_grid_threads": summary}
+           "by_kernel_grid": summary}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
