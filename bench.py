@@ -71,12 +71,13 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--object-gib", type=float, default=8.0, help="object bytes per GPU (GiB)")
     ap.add_argument("--chunk", type=int, default=32 << 20, help="chunk (leaf) bytes; default 32 MiB")
-    ap.add_argument("--no-sweep", action="store_true")
+    ap.add_argument("--sweep", action="store_true", help="also run the chunk-size sweep (N=1)")
+    ap.add_argument("--no-sweep", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
-    ap.add_argument("--sweep-modes", action="store_true", help="sweep both leaf kernels (wide, latency)")
+    ap.add_argument("--sweep-modes", action="store_true", help="sweep every leaf kernel (wide, latency, pair)")
     ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = CPU exchange (rehearsal on one GPU)")
@@ -272,7 +273,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         t1 = time.perf_counter()
         out["e2e"] = {"pinned_host_gibs": round(length / (t1 - t0) / (1 << 30), 4),
                       "root_matches": r.hex() == root_hex}
-    if not args.no_sweep:
+    if args.sweep and not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
         modes = ["wide", "latency", "pair"] if args.sweep_modes else ["auto"]

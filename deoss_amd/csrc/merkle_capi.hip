@@ -232,18 +232,44 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // Measured (profiles/r01_bench_modes.log, r01_crossover.log): the latency kernels win while
 // every workgroup gets a CU of its own (one consumer wave per SIMD); past that, one lane per
 // leaf with >= 2 waves per SIMD wins.
-int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n, bool table) {
-    if (table) return DM_LEAF_WIDE;
+int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
     if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
     if (ceil_div(n, dm::kPairLeaves) <= (uint64_t)d.cus) return DM_LEAF_PAIR;
     if (ceil_div(n, dm::kLatLeaves) <= (uint64_t)d.cus) return DM_LEAF_LATENCY;
     return DM_LEAF_WIDE;
 }
 
+template <bool TABLE, bool ALIGNED>
+void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
+    const uint64_t n = la.nleaves;
+    if (kind == DM_LEAF_PAIR)
+        hipLaunchKernelGGL((dm::leaf_kernel_pair<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
+                           dim3(dm::kLatThreads), 0, s, la);
+    else if (kind == DM_LEAF_LATENCY)
+        hipLaunchKernelGGL((dm::leaf_kernel_lat<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kLatLeaves)),
+                           dim3(dm::kLatThreads), 0, s, la);
+    else
+        hipLaunchKernelGGL((dm::leaf_kernel<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock),
+                           0, s, la);
+}
+
+// Launch the chosen leaf kernel (K1 / K1L / K1P) over la's leaves.
+int launch_leaves(dm_ctx* c, hipStream_t s, const dm::LeafArgs& la, bool table, bool aligned, int kind) {
+    if (table) {
+        if (aligned) launch_leaves_t<true, true>(s, la, kind);
+        else launch_leaves_t<true, false>(s, la, kind);
+    } else {
+        if (aligned) launch_leaves_t<false, true>(s, la, kind);
+        else launch_leaves_t<false, false>(s, la, kind);
+    }
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
 int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool aligned, int levels,
              uint8_t* dst, uint64_t* nout, uint8_t* leaf_dig) {
     const uint64_t n = la.nleaves;
-    const int kind = pick_leaf_kernel(c, d, n, table);
+    const int kind = pick_leaf_kernel(c, d, n);
     const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
     const uint32_t fuse_max = kind == DM_LEAF_PAIR ? dm::kPairFuseMax
                               : kind == DM_LEAF_LATENCY ? dm::kLatFuseMax : dm::kLeafFuseMax;
@@ -267,25 +293,7 @@ int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool
     }
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    if (kind == DM_LEAF_PAIR) {
-        const uint32_t grid = (uint32_t)ceil_div(n, dm::kPairLeaves);
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel_pair<true>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel_pair<false>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
-    } else if (kind == DM_LEAF_LATENCY) {
-        const uint32_t grid = (uint32_t)ceil_div(n, dm::kLatLeaves);
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel_lat<true>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel_lat<false>), dim3(grid), dim3(dm::kLatThreads), 0, s, la);
-    } else {
-        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
-        if (table) {
-            if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-            else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        } else {
-            if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-            else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        }
-    }
-    HIP_TRY(hipGetLastError());
+    RC_TRY(launch_leaves(c, s, la, table, aligned, kind));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     if (L1 == 0 && leaf_dig != nullptr && leaf_dig != dst)
         HIP_TRY(hipMemcpyAsync(leaf_dig, dst, n * 32, hipMemcpyDeviceToDevice, s));
@@ -373,10 +381,7 @@ int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, cons
     la.digests = d.leaves.u8();
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    const uint32_t grid = (uint32_t)ceil_div(T, dm::kBlock);
-    if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-    else hipLaunchKernelGGL((dm::leaf_kernel<true, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-    HIP_TRY(hipGetLastError());
+    RC_TRY(launch_leaves(c, s, la, true, aligned, pick_leaf_kernel(c, d, T)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, roots));
     if (tr) HIP_TRY(hipEventRecord(tr[2], s));
@@ -444,9 +449,10 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         pinned = attr.type == hipMemoryTypeHost;
     (void)hipGetLastError();   // clear the error of an unregistered pointer
     const bool aligned = (chunk % 16) == 0;
-    // Many leaves: hashing runs at >= 100x the PCIe rate, so copy then hash in one launch.
-    // Few large leaves (latency-bound hashing): stripes keep every leaf in flight while copying.
-    const bool contiguous = n >= 4096 || len <= kStripeBudget;
+    // Many leaves (wide kernel): hashing runs far above the PCIe rate, so copy then hash in one
+    // launch.  Fewer, larger leaves (latency-bound hashing): stripes keep every leaf in flight
+    // while the next stripe is copied.
+    const bool contiguous = pick_leaf_kernel(c, d, n) == DM_LEAF_WIDE || len <= kStripeBudget;
     dm::LeafArgs la{};
     la.pitch = chunk;
     la.leaf_len = chunk;
@@ -478,11 +484,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         la.base = d.data.u8();
         la.nleaves = n;
         la.byte_end = ~0ull;
-        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        HIP_TRY(hipGetLastError());
-        return DM_OK;
+        return launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, n));
     }
     // striped: W bytes of every leaf per step (W multiple of 64), state carried in HBM
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
@@ -527,10 +529,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         la.byte_off = b0;
         la.byte_end = b0 + w;
         la.state = state;
-        const uint32_t grid = (uint32_t)ceil_div(n, dm::kBlock);
-        if (aligned) hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        else hipLaunchKernelGGL((dm::leaf_kernel<false, false>), dim3(grid), dim3(dm::kBlock), 0, s, la);
-        HIP_TRY(hipGetLastError());
+        RC_TRY(launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, n)));
     }
     return DM_OK;
 }
@@ -764,7 +763,7 @@ int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
 int dm_leaf_kernel_for(dm_ctx* ctx, uint64_t nleaves) {
     if (!ctx) return DM_ERR_INVALID;
     std::lock_guard<std::mutex> lk(ctx->mu);
-    return pick_leaf_kernel(ctx, ctx->devs[0], nleaves, false);
+    return pick_leaf_kernel(ctx, ctx->devs[0], nleaves);
 }
 
 int dm_set_timing(dm_ctx* ctx, int enable) {
@@ -915,9 +914,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
     la.nleaves = n;
     la.byte_end = ~0ull;
     la.digests = d.leaves.u8();
-    hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock), 0,
-                       d.stream, la);
-    HIP_TRY(hipGetLastError());
+    RC_TRY(launch_leaves(c, d.stream, la, true, true, pick_leaf_kernel(c, d, n)));
     return reduce_leaves_to_host(c, d, n, leaf_out, root);
 }
 

@@ -151,44 +151,84 @@ __device__ __forceinline__ uint32_t lds_reduce(uint32_t (*a)[8], uint32_t (*b)[8
     return cnt;
 }
 
+// One leaf as seen by one launch: its bytes inside the stripe [byte_off, byte_end) (single
+// shot: the whole leaf), how many full blocks that is, and whether the leaf ends here.
+struct LeafView {
+    const uint8_t* p;   // first byte of this launch's part of the leaf
+    uint64_t len;       // total leaf length (for the padding)
+    uint64_t have;      // bytes of the leaf inside the stripe
+    uint64_t nb;        // full 64-byte blocks to absorb in this launch
+    bool fin;           // leaf ends inside this stripe: pad and emit the digest
+    bool active;
+};
+
+template <bool TABLE>
+__device__ __forceinline__ LeafView leaf_view(const LeafArgs& a, uint64_t i) {
+    LeafView v{};
+    v.active = i < a.nleaves;
+    if (!v.active) {
+        v.p = a.base;
+        return v;
+    }
+    if constexpr (TABLE) {
+        v.p = reinterpret_cast<const uint8_t*>(a.addrs[i]);
+        v.len = a.lens[i];
+    } else {
+        v.p = a.base + i * a.pitch;
+        v.len = (i + 1 == a.nleaves) ? a.last_len : a.leaf_len;
+    }
+    const uint64_t b0 = a.byte_off;
+    const uint64_t end = v.len < a.byte_end ? v.len : a.byte_end;
+    v.have = end > b0 ? end - b0 : 0;
+    v.fin = (b0 < v.len && v.len <= a.byte_end) || (v.len == 0 && b0 == 0);
+    v.nb = v.have / 64;   // not finishing: the stripe holds whole blocks only
+    return v;
+}
+
+__device__ __forceinline__ void load_or_init_state(const LeafArgs& a, uint64_t i, uint32_t (&st)[8]) {
+    if (a.state != nullptr && a.byte_off != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) st[k] = a.state[i * 8 + k];
+    } else {
+        init_state(st);
+    }
+}
+
+// Finish a leaf after its full blocks: pad + digest, or save the chaining state for the next stripe.
+template <bool ALIGNED>
+__device__ __forceinline__ void leaf_epilogue(const LeafArgs& a, uint64_t i, const LeafView& v, uint32_t (&st)[8]) {
+    if (v.fin) {
+        absorb_tail<ALIGNED>(st, v.p + 64 * v.nb, (uint32_t)(v.have - 64 * v.nb), v.len);
+        if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+    } else if (a.state != nullptr && v.have != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) a.state[i * 8 + k] = st[k];
+    }
+}
+
+// Largest value over the 64 lanes of the wave (wave-uniform result).
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
 // K1: leaf SHA-256, one lane per leaf; optionally fused with the first tree levels.
 template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void leaf_kernel(LeafArgs a) {
     __shared__ uint32_t lds_a[kBlock][8];
     __shared__ uint32_t lds_b[kBlock / 2][8];
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    const bool active = i < a.nleaves;
+    const LeafView v = leaf_view<TABLE>(a, i);
+    const bool active = v.active;
     uint32_t st[8];
     if (active) {
-        const uint8_t* p;
-        uint64_t len;
-        if constexpr (TABLE) {
-            p = reinterpret_cast<const uint8_t*>(a.addrs[i]);
-            len = a.lens[i];
-        } else {
-            p = a.base + i * a.pitch;
-            len = (i + 1 == a.nleaves) ? a.last_len : a.leaf_len;
-        }
-        // bytes of this leaf inside the stripe [byte_off, byte_end)
-        const uint64_t b0 = a.byte_off;
-        const uint64_t end = len < a.byte_end ? len : a.byte_end;
-        const uint64_t have = end > b0 ? end - b0 : 0;
-        const bool finalize = (b0 < len && len <= a.byte_end) || (len == 0 && b0 == 0);
-        if (a.state != nullptr && b0 != 0) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) st[k] = a.state[i * 8 + k];
-        } else {
-            init_state(st);
-        }
-        const uint64_t nb = finalize ? have / 64 : have / 64;
-        absorb_blocks<ALIGNED>(st, p, nb);
-        if (finalize) {
-            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(have - 64 * nb), len);
-            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
-        } else if (a.state != nullptr && have != 0) {
-#pragma unroll
-            for (int k = 0; k < 8; k++) a.state[i * 8 + k] = st[k];
-        }
+        load_or_init_state(a, i, st);
+        absorb_blocks<ALIGNED>(st, v.p, v.nb);
+        leaf_epilogue<ALIGNED>(a, i, v, st);
     }
     if (a.fuse_levels == 0) return;   // uniform across the grid
     const uint64_t first = (uint64_t)blockIdx.x * kBlock;
@@ -270,7 +310,7 @@ __device__ __forceinline__ void schedule_to_lds(uint32_t (&w)[16], uint4 (*kw)[k
     }
 }
 
-template <bool ALIGNED>
+template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
     __shared__ uint4 ring[kLatRing][16][kLatLeaves];
     __shared__ uint32_t lds_a[kLatLeaves][8];
@@ -280,36 +320,33 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < kLatLeaves;
     const uint64_t first = (uint64_t)blockIdx.x * kLatLeaves;
     const uint64_t i = first + lane;
-    const bool active = i < a.nleaves;
-    const uint64_t len = active ? ((i + 1 == a.nleaves) ? a.last_len : a.leaf_len) : 0;
-    const uint64_t nb = len / 64;
-    // trip count shared by both waves: only the global last leaf may be shorter
-    const uint64_t NB = (first + 1 < a.nleaves) ? a.leaf_len / 64 : a.last_len / 64;
-    const uint8_t* p = a.base + (active ? i : 0) * a.pitch;
-    uint32_t st[8];
+    const LeafView v = leaf_view<TABLE>(a, i);
+    // trip count shared by both waves (each computes the same maximum over the 64 leaves)
+    const uint64_t NB = wave_max_u64(v.nb);
     if (producer) {
         Blk cur;
-        if (nb > 0) cur = load_block<ALIGNED>(p);
+        if (v.nb > 0) cur = load_block<ALIGNED>(v.p);
         for (uint64_t b = 0; b < NB; b++) {
-            if (b < nb) {
+            if (b < v.nb) {
                 uint32_t w[16];
                 block_words(cur, w);
-                if (b + 1 < nb) cur = load_block<ALIGNED>(p + 64 * (b + 1));
+                if (b + 1 < v.nb) cur = load_block<ALIGNED>(v.p + 64 * (b + 1));
                 schedule_to_lds(w, ring[b % kLatRing], lane);
             }
             __syncthreads();   // slot b full  /  slot b-1 free
         }
         __syncthreads();       // pairs with the consumer's final-iteration barrier
     } else {
-        init_state(st);
+        uint32_t st[8];
+        if (v.active) load_or_init_state(a, i, st);
+        else init_state(st);
         __syncthreads();       // wait for slot 0
         for (uint64_t b = 0; b < NB; b++) {
-            if (b < nb) rounds_from_kw(st, ring[b % kLatRing], lane);
+            if (b < v.nb) rounds_from_kw(st, ring[b % kLatRing], lane);
             __syncthreads();   // slot b consumed; slot b+1 full
         }
-        if (active) {
-            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(len - 64 * nb), len);
-            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+        if (v.active) {
+            leaf_epilogue<ALIGNED>(a, i, v, st);
 #pragma unroll
             for (int k = 0; k < 8; k++) lds_a[lane][k] = st[k];
         }
@@ -320,11 +357,11 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
     uint32_t (*res)[8];
     const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
     if (threadIdx.x < out_cnt) {
-        uint32_t v[8];
+        uint32_t o8[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = res[threadIdx.x][k];
+        for (int k = 0; k < 8; k++) o8[k] = res[threadIdx.x][k];
         const uint64_t o = (uint64_t)blockIdx.x * (kLatLeaves >> a.fuse_levels) + threadIdx.x;
-        store_digest(a.level_out + 32 * o, v);
+        store_digest(a.level_out + 32 * o, o8);
     }
 }
 
@@ -380,7 +417,7 @@ __device__ __forceinline__ void pair_rounds_from_kw(uint32_t (&x)[4], const uint
     x[0] += x4; x[1] += x5; x[2] += x6; x[3] += x7;
 }
 
-template <bool ALIGNED>
+template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
     __shared__ uint4 ring[kLatRing][16][kLatLeaves];
     __shared__ uint32_t lds_a[kPairLeaves][8];
@@ -391,24 +428,21 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
     const uint32_t c = lane >> 1;                           // leaf within the workgroup
     const uint64_t first = (uint64_t)blockIdx.x * kPairLeaves;
     const uint64_t i = first + c;
-    const bool active = i < a.nleaves;
-    const uint64_t len = active ? ((i + 1 == a.nleaves) ? a.last_len : a.leaf_len) : 0;
-    const uint64_t nb = len / 64;
-    const uint64_t NB = (first + 1 < a.nleaves) ? a.leaf_len / 64 : a.last_len / 64;
-    const uint8_t* p = a.base + (active ? i : 0) * a.pitch;
+    const LeafView v = leaf_view<TABLE>(a, i);
+    const uint64_t NB = wave_max_u64(v.nb);
     if (producer) {
         // even lanes compute leaf c's K+W; odd lanes publish zeros (the B half adds no K+W)
         Blk cur;
-        if (nb > 0 && !lane_b) cur = load_block<ALIGNED>(p);
+        if (v.nb > 0 && !lane_b) cur = load_block<ALIGNED>(v.p);
         for (uint64_t b = 0; b < NB; b++) {
-            if (b < nb) {
+            if (b < v.nb) {
                 uint32_t w[16];
                 block_words(cur, w);
-                if (b + 1 < nb && !lane_b) cur = load_block<ALIGNED>(p + 64 * (b + 1));
+                if (b + 1 < v.nb && !lane_b) cur = load_block<ALIGNED>(v.p + 64 * (b + 1));
                 uint4 (*kw)[kLatLeaves] = ring[b % kLatRing];
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
-                    uint32_t v[4];
+                    uint32_t u[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) {
                         const int t = 4 * q + j;
@@ -419,9 +453,9 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
                             wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
                             w[t & 15] = wt;
                         }
-                        v[j] = lane_b ? 0u : kSha256K[t] + wt;
+                        u[j] = lane_b ? 0u : kSha256K[t] + wt;
                     }
-                    kw[q][lane] = make_uint4(v[0], v[1], v[2], v[3]);
+                    kw[q][lane] = make_uint4(u[0], u[1], u[2], u[3]);
                 }
             }
             __syncthreads();
@@ -431,12 +465,15 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
         // per-lane constants of the packed round
         const uint32_t sh1 = lane_b ? 2 : 6, sh2 = lane_b ? 13 : 11, sh3 = lane_b ? 22 : 25;
         const uint32_t msk = lane_b ? 0u : ~0u;
+        uint32_t st0[8];
+        if (v.active) load_or_init_state(a, i, st0);
+        else init_state(st0);
         uint32_t x[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = lane_b ? kIV[k] : kIV[4 + k];
+        for (int k = 0; k < 4; k++) x[k] = lane_b ? st0[k] : st0[4 + k];
         __syncthreads();
         for (uint64_t b = 0; b < NB; b++) {
-            if (b < nb) pair_rounds_from_kw(x, ring[b % kLatRing], lane, sh1, sh2, sh3, msk, lane_b);
+            if (b < v.nb) pair_rounds_from_kw(x, ring[b % kLatRing], lane, sh1, sh2, sh3, msk, lane_b);
             __syncthreads();
         }
         // reassemble the full state on lane A: (a,b,c,d) from lane B, (e,f,g,h) own
@@ -447,9 +484,8 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
             st[k] = lane_b ? x[k] : other;
             st[4 + k] = lane_b ? other : x[k];
         }
-        if (active && !lane_b) {
-            absorb_tail<ALIGNED>(st, p + 64 * nb, (uint32_t)(len - 64 * nb), len);
-            if (a.digests != nullptr) store_digest(a.digests + 32 * i, st);
+        if (v.active && !lane_b) {
+            leaf_epilogue<ALIGNED>(a, i, v, st);
 #pragma unroll
             for (int k = 0; k < 8; k++) lds_a[c][k] = st[k];
         }
@@ -460,11 +496,11 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
     uint32_t (*res)[8];
     const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
     if (threadIdx.x < out_cnt) {
-        uint32_t v[8];
+        uint32_t o8[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = res[threadIdx.x][k];
+        for (int k = 0; k < 8; k++) o8[k] = res[threadIdx.x][k];
         const uint64_t o = (uint64_t)blockIdx.x * (kPairLeaves >> a.fuse_levels) + threadIdx.x;
-        store_digest(a.level_out + 32 * o, v);
+        store_digest(a.level_out + 32 * o, o8);
     }
 }
 

@@ -28,8 +28,8 @@ COUNTS = os.path.join(HERE, "isa_counts.json")
 SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0}
 KERNELS = {
     "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", 1),
-    "latency": ("_ZN2dm15leaf_kernel_latILb1EEEvNS_8LeafArgsE", 2),
-    "pair": ("_ZN2dm16leaf_kernel_pairILb1EEEvNS_8LeafArgsE", 4),
+    "latency": ("_ZN2dm15leaf_kernel_latILb0ELb1EEEvNS_8LeafArgsE", 2),
+    "pair": ("_ZN2dm16leaf_kernel_pairILb0ELb1EEEvNS_8LeafArgsE", 4),
 }
 K1_SYMBOL = KERNELS["wide"][0]
 

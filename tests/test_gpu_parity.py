@@ -89,22 +89,23 @@ def test_new_hash_tree_errors_and_dup(tmp_path):
     assert eq and e is None
 
 
+@pytest.fixture(params=["wide", "latency", "pair"])
+def leaf_mode(request, ctx):
+    """Run a test under each leaf kernel: K1 (one lane per leaf), K1L (producer/consumer waves),
+    K1P (producer/consumer, rounds on lane pairs)."""
+    ctx.set_leaf_kernel(request.param)
+    yield request.param
+    ctx.set_leaf_kernel("auto")
+
+
 # ---------------------------------------------------------------- golden fixtures
-def test_golden_chunks(ctx, golden):
+def test_golden_chunks(ctx, golden, leaf_mode):
     for case in golden:
         if case["kind"] != "chunks":
             continue
         leaves, root = ctx.root_chunks(chunks_of(case))
         assert root.hex() == case["root"], case["name"]
         assert [leaves[32 * i:32 * i + 32].hex() for i in range(len(case["leaves"]))] == case["leaves"], case["name"]
-
-
-@pytest.fixture(params=["wide", "latency", "pair"])
-def leaf_mode(request, ctx):
-    """Run a test under each leaf kernel (K1 one-lane-per-leaf, K1L producer/consumer)."""
-    ctx.set_leaf_kernel(request.param)
-    yield request.param
-    ctx.set_leaf_kernel("auto")
 
 
 def test_golden_buffers_all_paths(ctx, golden, leaf_mode):
@@ -129,7 +130,7 @@ def test_golden_buffers_all_paths(ctx, golden, leaf_mode):
         assert ctx.root_device(ptr, len(buf), chunk).hex() == case["root"]
 
 
-def test_golden_batch(ctx, golden):
+def test_golden_batch(ctx, golden, leaf_mode):
     torch = _torch()
     for case in golden:
         if case["kind"] != "batch":
@@ -144,6 +145,23 @@ def test_golden_batch(ctx, golden):
         torch.cuda.synchronize()
         got = bytes(out.cpu().numpy())
         assert [got[32 * i:32 * i + 32].hex() for i in range(len(objs))] == case["roots"]
+
+
+def test_batch_ragged_objects(ctx, oracle_lib, leaf_mode):
+    """Table mode with objects of many lengths (ragged leaf counts inside one workgroup)."""
+    torch = _torch()
+    import random
+    rnd = random.Random(7)
+    lens = [rnd.choice([1, 63, 64, 65, 200, 4096, 4097, 9000, 40000, 70001]) for _ in range(300)]
+    objs = [oracle_lib.splitmix_bytes(n, 1000 + i) for i, n in enumerate(lens)]
+    wants = [oracle_lib.root_buffer(o, 4096)[1] for o in objs]
+    assert ctx.root_batch(objs, 4096) == wants
+    keep = [dev_bytes(o) for o in objs]
+    out = torch.zeros(32 * len(objs), dtype=torch.uint8, device="cuda")
+    ctx.root_batch_device_async([p for _, p in keep], lens, 4096, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = bytes(out.cpu().numpy())
+    assert [got[32 * i:32 * i + 32] for i in range(len(objs))] == wants
 
 
 # ---------------------------------------------------------------- edge cases
@@ -228,7 +246,7 @@ def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world, leaf_mode):
 
 # ---------------------------------------------------------------- host buffer e2e (stripes)
 @pytest.mark.parametrize("pinned", [False, True])
-def test_host_buffer_striped_large_leaves(ctx, oracle_lib, pinned):
+def test_host_buffer_striped_large_leaves(ctx, oracle_lib, pinned, leaf_mode):
     """Few large leaves (> 256 MiB object): the striped H2D path with resumable leaf state."""
     torch = _torch()
     length, chunk = (300 << 20) + 12345, 64 << 20
@@ -239,7 +257,7 @@ def test_host_buffer_striped_large_leaves(ctx, oracle_lib, pinned):
     assert root == want and leaves == leaves_want
 
 
-def test_host_buffer_many_leaves(ctx, oracle_lib):
+def test_host_buffer_many_leaves(ctx, oracle_lib, leaf_mode):
     torch = _torch()
     length, chunk = (96 << 20) + 3, 16 << 10
     t = torch.empty(length, dtype=torch.uint8)
