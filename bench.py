@@ -76,6 +76,11 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
+    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream"],
+                    help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
+                         "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4])")
+    ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
+    ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
     ap.add_argument("--sweep-modes", action="store_true", help="sweep every leaf kernel (wide, latency, pair)")
     ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair"])
@@ -105,6 +110,8 @@ def main() -> None:
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
+    if args.workload != "object":
+        return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
     per_gpu = int(args.object_gib * (1 << 30))
     chunk = args.chunk
     total = per_gpu * world
@@ -232,6 +239,105 @@ def main() -> None:
         single = bytes(one.cpu().numpy()).hex()
         out["parity"] = {"sharded_root": root_hex, "single_gpu_root": single, "bit_exact": single == root_hex}
         del full
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        barrier()
+        dist.destroy_process_group()
+
+
+def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
+    """configs[2] (batch: objects already in HBM) and configs[4] (stream: objects in host memory,
+    pinned staging + H2D inside the timed region).  Objects are split across ranks with no
+    exchange (each object's tree is independent)."""
+    from deoss_amd import MerkleContext
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    obj = int(args.object_mib * (1 << 20))
+    nobj = args.objects
+    chunk = args.chunk
+    ctx = MerkleContext(devices=[dev_index])
+    ctx.set_leaf_kernel(args.leaf_kernel)
+    sptr = torch.cuda.current_stream().cuda_stream
+    seed0 = SEED + 1000 * (rank + 1)
+    total_local = obj * nobj
+    pitch = (obj + 255) // 256 * 256
+    buf = torch.empty(pitch * nobj + 64, dtype=torch.uint8, device=device)
+    for j in range(nobj):   # object j of this rank: splitmix64 stream with its own seed
+        ctx.fill_synthetic_async(buf.data_ptr() + j * pitch, 0, (obj + 7) // 8 * 8, seed0 + j, sptr)
+    ptrs = [buf.data_ptr() + j * pitch for j in range(nobj)]
+    lens = [obj] * nobj
+    roots = torch.zeros(32 * nobj, dtype=torch.uint8, device=device)
+    host = None
+    if args.workload == "stream":
+        host = torch.empty(pitch * nobj, dtype=torch.uint8, pin_memory=True)
+        host.copy_(buf[:pitch * nobj])
+        torch.cuda.synchronize()
+        del buf
+        import ctypes
+        hptrs = [host.data_ptr() + j * pitch for j in range(nobj)]
+
+        def step():
+            n = len(hptrs)
+            P = (ctypes.c_void_p * n)(*hptrs)
+            L = (ctypes.c_uint64 * n)(*lens)
+            out = ctypes.create_string_buffer(32 * n)
+            ctx._check(ctx._L.dm_root_batch(ctx._h, P, L, n, chunk, out), "dm_root_batch")
+            return out.raw
+    else:
+        def step():
+            ctx.root_batch_device_async(ptrs, lens, chunk, roots.data_ptr(), sptr)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier() if gloo else dist.barrier(device_ids=[dev_index])
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = step()
+    barrier()
+    t1 = time.perf_counter()
+    ncalls, k1_ms_sum, call_ms_sum, _ = ctx.timing_summary()
+    ctx.set_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    got = last if args.workload == "stream" else bytes(roots.cpu().numpy())
+    # parity: every root of this rank against the CPU oracle (16 threads, untimed)
+    from oracle import Oracle
+    orc = Oracle()
+    src = host if host is not None else None
+    mism = 0
+    check = min(nobj, 512)
+    for j in range(check):
+        if src is not None:
+            addr = src.data_ptr() + j * pitch
+            _, want = orc.root_buffer_ptr(addr, obj, chunk, nthreads=1)
+        else:
+            want = orc.root_buffer(orc.splitmix_bytes(obj, seed0 + j), chunk)[1]
+        mism += want != got[32 * j:32 * j + 32]
+    leaves = (obj + chunk - 1) // chunk * nobj
+    kind = ctx.leaf_kernel_for(leaves)
+    out = {
+        "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling" if args.workload == "batch"
+        else "host-resident GiB/s hashed to Merkle roots (pinned H2D inside the timed region)",
+        "value": round(total_local * world * args.steps / elapsed / (1 << 30), 4), "unit": "GiB/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic splitmix64 objects",
+        "config": {"workload": f"{nobj} objects x {obj} B per GPU ({args.workload}), chunk {chunk}",
+                   "objects_per_gpu": nobj, "object_bytes": obj, "chunk": chunk, "leaf_kernel": kind},
+        "k1_avg_ms": round(k1_ms_sum / max(ncalls, 1), 4), "call_avg_ms": round(call_ms_sum / max(ncalls, 1), 4),
+        "parity": {"checked_objects": check, "mismatches": int(mism), "bit_exact": mism == 0},
+    }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

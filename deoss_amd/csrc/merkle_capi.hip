@@ -401,6 +401,32 @@ int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens
     HIP_TRY(d.data.ensure(std::max<uint64_t>(total, kAlign)));
     addr.resize(n);
     for (uint64_t i = 0; i < n; i++) addr[i] = reinterpret_cast<uint64_t>(d.data.u8() + off[i]);
+    // Pinned sources (every chunk in page-locked host memory): async copies straight from the
+    // caller's buffers, coalescing runs that are contiguous on both sides with no padding between
+    // them (so a copy never reads a host byte outside the caller's chunks).
+    bool all_pinned = true;
+    for (uint64_t i = 0; i < n && all_pinned; i++) {
+        if (lens[i] == 0) continue;
+        hipPointerAttribute_t attr{};
+        all_pinned = hipPointerGetAttributes(&attr, ptrs[i]) == hipSuccess && attr.type == hipMemoryTypeHost;
+    }
+    (void)hipGetLastError();
+    if (all_pinned) {
+        uint64_t i = 0;
+        while (i < n) {
+            if (lens[i] == 0) { i++; continue; }
+            const uint8_t* h0 = static_cast<const uint8_t*>(ptrs[i]);
+            uint64_t j = i + 1;
+            while (j < n && lens[j] && lens[j - 1] % kAlign == 0 &&
+                   static_cast<const uint8_t*>(ptrs[j]) == static_cast<const uint8_t*>(ptrs[j - 1]) + lens[j - 1])
+                j++;
+            const uint64_t bytes = off[j - 1] - off[i] + lens[j - 1];
+            HIP_TRY(hipMemcpyAsync(d.data.u8() + off[i], h0, bytes, hipMemcpyHostToDevice, d.copy));
+            i = j;
+        }
+        HIP_TRY(hipStreamSynchronize(d.copy));
+        return DM_OK;
+    }
     HIP_TRY(d.stage[0].ensure(kStageBytes));
     HIP_TRY(d.stage[1].ensure(kStageBytes));
     int slot = 0;
