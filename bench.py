@@ -73,7 +73,8 @@ def main() -> None:
     ap.add_argument("--chunk", type=int, default=32 << 20, help="chunk (leaf) bytes; default 32 MiB")
     ap.add_argument("--sweep", action="store_true", help="also run the chunk-size sweep (N=1)")
     ap.add_argument("--no-sweep", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="also time the host-buffer path (N=1)")
+    ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--workload", default="object", choices=["object", "batch", "stream"],
@@ -351,7 +352,8 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     from oracle import Oracle   # CPU baseline / checker only
     orc = Oracle()
     host = None
-    if not args.no_cpu or not args.no_e2e:
+    do_e2e = args.e2e and not args.no_e2e
+    if not args.no_cpu or do_e2e:
         host = torch.empty(length, dtype=torch.uint8, pin_memory=True)
         host.copy_(buf[:length])
         torch.cuda.synchronize()
@@ -371,7 +373,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         }
         out["parity"] = {"gpu_root": root_hex, "cpu_root": cpu_root.hex(),
                          "bit_exact": cpu_root.hex() == root_hex and cpu_root_p == cpu_root}
-    if not args.no_e2e and host is not None:
+    if do_e2e and host is not None:
         # host pinned buffer -> H2D (overlapped) -> root -> 32 B back (the upload-handler path)
         ctx.root_buffer_ptr(host.data_ptr(), min(length, 64 << 20), chunk)   # warm staging
         t0 = time.perf_counter()

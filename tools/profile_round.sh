@@ -6,7 +6,7 @@ set -e
 tag=${1:-r01}; shift || true
 out=gpurun_out/prof_$tag
 mkdir -p $out
-args="--steps 2 --warmup 1 --no-cpu --no-e2e --sweep --sweep-modes $*"
+args="--steps 2 --warmup 1 --no-cpu --sweep --sweep-modes $*"
 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py $args > $out/bench_kt.json
 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o fetch --output-format csv -- python3 bench.py $args > $out/bench_fetch.json
 rocprofv3 --pmc WRITE_SIZE -d $out/write -o write --output-format csv -- python3 bench.py $args > $out/bench_write.json
