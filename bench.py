@@ -379,8 +379,17 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         t0 = time.perf_counter()
         _, r = ctx.root_buffer_ptr(host.data_ptr(), length, chunk)
         t1 = time.perf_counter()
+        pageable = torch.empty(length, dtype=torch.uint8)          # ordinary (pageable) host memory
+        pageable.copy_(host)
+        t2 = time.perf_counter()
+        _, r2 = ctx.root_buffer_ptr(pageable.data_ptr(), length, chunk)
+        t3 = time.perf_counter()
+        del pageable
         out["e2e"] = {"pinned_host_gibs": round(length / (t1 - t0) / (1 << 30), 4),
-                      "root_matches": r.hex() == root_hex}
+                      "pageable_host_gibs": round(length / (t3 - t2) / (1 << 30), 4),
+                      "root_matches": r.hex() == root_hex and r2.hex() == root_hex,
+                      "path": "host buffer -> (pinned ring | direct) H2D, striped, overlapped with the leaf "
+                              "kernel -> tree -> 32 B root back (dm_root_buffer)"}
     if args.sweep and not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)

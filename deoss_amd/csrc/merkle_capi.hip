@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -115,6 +116,9 @@ struct dm_ctx {
     std::string err;
     bool timing = false;
     int leaf_mode = DM_LEAF_AUTO;
+    // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-buffer objects through the
+    // multi-device path (partition, RCCL all-gather, compaction, finish) even with one device.
+    bool force_sharded = false;
 };
 
 namespace {
@@ -760,7 +764,9 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
             return rc;
         }
     }
-    if (ids.size() > 1) {
+    const char* fs = std::getenv("DEOSS_FORCE_SHARDED");
+    c->force_sharded = fs != nullptr && fs[0] == '1';
+    if (ids.size() > 1 || c->force_sharded) {
         c->comms.resize(ids.size());
         if (ncclCommInitAll(c->comms.data(), (int)ids.size(), ids.data()) != ncclSuccess) {
             c->comms.clear();
@@ -910,7 +916,7 @@ int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, 
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    if (c->devs.size() > 1 && ceil_div(len, chunk) >= 2 * c->devs.size())
+    if ((c->devs.size() > 1 || c->force_sharded) && ceil_div(len, chunk) >= 2 * c->devs.size())
         return root_buffer_multi(c, host, len, chunk, leaf_out, root);
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));

@@ -244,6 +244,26 @@ def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world, leaf_mode):
         assert bytes(root.cpu().numpy()) == want, (length, chunk, world)
 
 
+def test_single_process_sharded_path(oracle_lib):
+    """dm_create's multi-device path (aligned block partition, ncclAllGather of subtree roots,
+    compaction, final levels) forced on the one GPU of this box via DEOSS_FORCE_SHARDED."""
+    from deoss_amd import MerkleContext
+    os.environ["DEOSS_FORCE_SHARDED"] = "1"
+    try:
+        c = MerkleContext()
+    finally:
+        del os.environ["DEOSS_FORCE_SHARDED"]
+    try:
+        for length, chunk in [(1000 * 4096 + 7, 4096), (3 * 64, 64), (5000, 1000), ((1 << 20) + 3, 1 << 14)]:
+            host = oracle_lib.splitmix_bytes(length, length + 1)
+            lw, want = oracle_lib.root_buffer(host, chunk)
+            leaves, root = c.root_buffer(host, chunk, want_leaves=True)
+            assert root == want, (length, chunk)
+            assert leaves == lw, (length, chunk)
+    finally:
+        c.close()
+
+
 # ---------------------------------------------------------------- host buffer e2e (stripes)
 @pytest.mark.parametrize("pinned", [False, True])
 def test_host_buffer_striped_large_leaves(ctx, oracle_lib, pinned, leaf_mode):
