@@ -77,9 +77,11 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
-    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream"],
+    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
-                         "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4])")
+                         "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
+                         "upload: one object fed in pieces through dm_stream (hash while receiving)")
+    ap.add_argument("--piece-kib", type=int, default=1024, help="upload: bytes per dm_stream_write (KiB)")
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
     ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
@@ -111,6 +113,8 @@ def main() -> None:
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
+    if args.workload == "upload":
+        return run_upload(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload != "object":
         return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
     per_gpu = int(args.object_gib * (1 << 30))
@@ -245,6 +249,55 @@ def main() -> None:
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #1: the upload body arrives in pieces; dm_stream hashes whole leaves while later pieces
+    are still being written.  Timed from open to the root; the tail (last write -> root) is the
+    latency a handler sees after the body ends."""
+    from deoss_amd import MerkleContext
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    length = int(args.object_gib * (1 << 30))
+    chunk = args.chunk
+    piece = args.piece_kib << 10
+    ctx = MerkleContext(devices=[dev_index])
+    ctx.set_leaf_kernel(args.leaf_kernel)
+    orc = Oracle()
+    host = torch.empty(length, dtype=torch.uint8)            # pageable, like a Go []byte body
+    orc.fill_splitmix_ptr(host.data_ptr(), 0, length // 8 * 8, SEED)
+    base = host.data_ptr()
+
+    def one():
+        st = ctx.open_stream(chunk)
+        t0 = time.perf_counter()
+        for off in range(0, length, piece):
+            st.write((base + off, min(piece, length - off)))
+        t1 = time.perf_counter()
+        _, r = st.close()
+        t2 = time.perf_counter()
+        return r, t2 - t0, t2 - t1
+
+    for _ in range(args.warmup):
+        one()
+    times, tails, root = [], [], None
+    for _ in range(args.steps):
+        root, t, tail = one()
+        times.append(t)
+        tails.append(tail)
+    _, want = orc.root_buffer_ptr(base, length, chunk, nthreads=min(16, os.cpu_count() or 1))
+    tavg = sum(times) / len(times)
+    out = {
+        "metric": "host-buffer upload GiB/s hashed to Merkle root while receiving (dm_stream, pageable pieces)",
+        "value": round(length / tavg / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(tavg * 1e3, 3), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "u32", "data": "synthetic splitmix64 object",
+        "config": {"workload": f"{length} B object written in {piece} B pieces, chunk {chunk}",
+                   "leaf_kernel": ctx.leaf_kernel_for(min(64, (length + chunk - 1) // chunk))},
+        "tail_ms_after_last_write": round(sum(tails) / len(tails) * 1e3, 3),
+        "parity": {"root": root.hex(), "cpu_root": want.hex(), "bit_exact": root == want},
+    }
+    print(json.dumps(out), flush=True)
 
 
 def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):

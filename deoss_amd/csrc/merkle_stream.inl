@@ -1,0 +1,293 @@
+// merkle_stream.inl -- incremental Merkle root of one object whose bytes arrive in pieces
+// (hash the upload body while it is received instead of after
+// node/objectHandler.go:248-266 / node/fileHandler.go:899-937 have written it to a temp file).
+// Included by merkle_capi.hip (shares its internal helpers).
+//
+// Host pieces -> pinned staging (2 slots) -> H2D into leaf-aligned device segments (copy
+// stream) -> as soon as enough whole leaves are on the device, a leaf-kernel launch over them
+// on one of kStreamLanes compute streams (so several batches hash concurrently while more bytes
+// arrive) -> at close, the last partial leaf, then the tree over all leaf digests.
+
+namespace {
+
+constexpr uint64_t kStreamStage = 64ull << 20;   // pinned staging slot
+constexpr int kStreamLanes = 4;                  // concurrent compute streams per object
+constexpr uint64_t kStreamMinLeaves = 64;        // launch when this many whole leaves wait...
+constexpr uint64_t kStreamMinBytes = 1ull << 30; // ...or this many bytes of them
+
+struct StreamSeg {
+    DevBuf data;      // seg_leaves * chunk bytes
+    DevBuf digests;   // seg_leaves * 32 bytes
+};
+
+}  // namespace
+
+struct dm_stream {
+    dm_ctx* c = nullptr;
+    int dev = 0;
+    uint64_t chunk = 0;
+    uint64_t seg_leaves = 0;
+    std::vector<StreamSeg*> segs;
+    PinnedBuf stage[2];
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
+    bool busy[2] = {false, false};
+    int slot = 0;
+    uint64_t fill = 0;
+    hipStream_t copy = nullptr;
+    hipStream_t comp[kStreamLanes] = {};
+    hipEvent_t ev_copy = nullptr;
+    hipEvent_t ev_comp[kStreamLanes] = {};
+    int next_comp = 0;
+    uint64_t received = 0;   // bytes handed to dm_stream_write
+    uint64_t on_device = 0;  // bytes whose H2D is enqueued
+    uint64_t launched = 0;   // leaves whose hashing is enqueued
+    int kind = DM_LEAF_PAIR;
+    std::string err;
+};
+
+namespace {
+
+int sfail(dm_stream* st, int code, const char* what, hipError_t e) {
+    char buf[512];
+    snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    st->err = buf;
+    return code;
+}
+
+#define SHIP(expr)                                                                               \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess) return sfail(st, e_ == hipErrorOutOfMemory ? DM_ERR_NOMEM : DM_ERR_HIP, #expr, e_); \
+    } while (0)
+
+int stream_seg_for(dm_stream* st, uint64_t leaf, StreamSeg** out) {
+    const uint64_t si = leaf / st->seg_leaves;
+    while (st->segs.size() <= si) {
+        StreamSeg* g = new StreamSeg();
+        st->segs.push_back(g);
+        SHIP(g->data.ensure(st->seg_leaves * st->chunk));
+        SHIP(g->digests.ensure(st->seg_leaves * 32));
+    }
+    *out = st->segs[si];
+    return DM_OK;
+}
+
+// Enqueue hashing of leaves [launched, upto); the leaf upto-1 may be the short last one.
+int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
+    if (upto <= st->launched) return DM_OK;
+    SHIP(hipEventRecord(st->ev_copy, st->copy));
+    const int k = st->next_comp++ % kStreamLanes;
+    hipStream_t s = st->comp[k];
+    SHIP(hipStreamWaitEvent(s, st->ev_copy, 0));
+    while (st->launched < upto) {
+        StreamSeg* g;
+        int rc = stream_seg_for(st, st->launched, &g);
+        if (rc != DM_OK) return rc;
+        const uint64_t first = st->launched % st->seg_leaves;
+        const uint64_t n = std::min(upto - st->launched, st->seg_leaves - first);
+        dm::LeafArgs la{};
+        la.base = g->data.u8() + first * st->chunk;
+        la.pitch = st->chunk;
+        la.leaf_len = st->chunk;
+        la.last_len = (st->launched + n == upto) ? last_len : st->chunk;
+        la.nleaves = n;
+        la.byte_end = ~0ull;
+        la.digests = g->digests.u8() + first * 32;
+        const int kind = pick_leaf_kernel(st->c, st->c->devs[st->dev], n);
+        if (kind == DM_LEAF_PAIR)
+            hipLaunchKernelGGL((dm::leaf_kernel_pair<false, true>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
+                               dim3(dm::kLatThreads), 0, s, la);
+        else if (kind == DM_LEAF_LATENCY)
+            hipLaunchKernelGGL((dm::leaf_kernel_lat<false, true>), dim3((uint32_t)ceil_div(n, dm::kLatLeaves)),
+                               dim3(dm::kLatThreads), 0, s, la);
+        else
+            hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock),
+                               0, s, la);
+        SHIP(hipGetLastError());
+        st->launched += n;
+    }
+    SHIP(hipEventRecord(st->ev_comp[k], s));
+    return DM_OK;
+}
+
+// Move the filled staging slot to the device and launch whatever whole leaves are ready.
+int stream_flush(dm_stream* st) {
+    if (st->fill == 0) return DM_OK;
+    const uint8_t* src = st->stage[st->slot].u8();
+    uint64_t pos = st->on_device, left = st->fill;
+    while (left) {
+        StreamSeg* g;
+        int rc = stream_seg_for(st, pos / st->chunk, &g);
+        if (rc != DM_OK) return rc;
+        const uint64_t seg_off = pos - (pos / st->chunk / st->seg_leaves) * st->seg_leaves * st->chunk;
+        const uint64_t room = st->seg_leaves * st->chunk - seg_off;
+        const uint64_t n = std::min(left, room);
+        SHIP(hipMemcpyAsync(g->data.u8() + seg_off, src, n, hipMemcpyHostToDevice, st->copy));
+        src += n;
+        pos += n;
+        left -= n;
+    }
+    SHIP(hipEventRecord(st->ev_stage[st->slot], st->copy));
+    st->busy[st->slot] = true;
+    st->on_device += st->fill;
+    st->slot ^= 1;
+    st->fill = 0;
+    const uint64_t ready = st->on_device / st->chunk;
+    const uint64_t pending = ready > st->launched ? ready - st->launched : 0;
+    if (pending >= kStreamMinLeaves || pending * st->chunk >= kStreamMinBytes)
+        return stream_launch(st, ready, st->chunk);
+    return DM_OK;
+}
+
+void stream_free(dm_stream* st) {
+    if (!st) return;
+    (void)hipSetDevice(st->c->devs[st->dev].id);
+    if (st->copy) (void)hipStreamSynchronize(st->copy);
+    for (int k = 0; k < kStreamLanes; k++)
+        if (st->comp[k]) (void)hipStreamSynchronize(st->comp[k]);
+    for (StreamSeg* g : st->segs) {
+        g->data.release();
+        g->digests.release();
+        delete g;
+    }
+    st->stage[0].release();
+    st->stage[1].release();
+    for (hipEvent_t e : {st->ev_stage[0], st->ev_stage[1], st->ev_copy})
+        if (e) (void)hipEventDestroy(e);
+    for (int k = 0; k < kStreamLanes; k++) {
+        if (st->ev_comp[k]) (void)hipEventDestroy(st->ev_comp[k]);
+        if (st->comp[k]) (void)hipStreamDestroy(st->comp[k]);
+    }
+    if (st->copy) (void)hipStreamDestroy(st->copy);
+    delete st;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
+    if (!ctx || !out || chunk == 0) return DM_ERR_INVALID;
+    *out = nullptr;
+    if (chunk % 16 != 0) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        return fail(ctx, DM_ERR_INVALID, "dm_stream: chunk must be a multiple of 16 bytes");
+    }
+    dm_stream* st = new dm_stream();
+    st->c = ctx;
+    st->chunk = chunk;
+    st->seg_leaves = std::max<uint64_t>(1, (1ull << 30) / chunk);
+    int rc = DM_OK;
+    do {
+        hipError_t e;
+        if ((e = hipSetDevice(ctx->devs[0].id)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "hipSetDevice", e); break; }
+        if ((e = hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "stream", e); break; }
+        for (int k = 0; k < kStreamLanes && rc == DM_OK; k++) {
+            if ((e = hipStreamCreateWithFlags(&st->comp[k], hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&st->ev_comp[k], hipEventDisableTiming)) != hipSuccess)
+                rc = sfail(st, DM_ERR_HIP, "stream", e);
+        }
+        if (rc != DM_OK) break;
+        if ((e = hipEventCreateWithFlags(&st->ev_copy, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&st->ev_stage[0], hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&st->ev_stage[1], hipEventDisableTiming)) != hipSuccess) {
+            rc = sfail(st, DM_ERR_HIP, "event", e);
+            break;
+        }
+        if ((e = st->stage[0].ensure(kStreamStage)) != hipSuccess || (e = st->stage[1].ensure(kStreamStage)) != hipSuccess) {
+            rc = sfail(st, DM_ERR_NOMEM, "pinned staging", e);
+            break;
+        }
+    } while (0);
+    if (rc != DM_OK) {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ctx->err = st->err;
+        stream_free(st);
+        return rc;
+    }
+    *out = st;
+    return DM_OK;
+}
+
+int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
+    if (!st || (!data && len)) return DM_ERR_INVALID;
+    SHIP(hipSetDevice(st->c->devs[st->dev].id));
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    while (len) {
+        if (st->fill == 0 && st->busy[st->slot]) {
+            SHIP(hipEventSynchronize(st->ev_stage[st->slot]));
+            st->busy[st->slot] = false;
+        }
+        const uint64_t take = std::min(len, kStreamStage - st->fill);
+        std::memcpy(st->stage[st->slot].u8() + st->fill, p, take);
+        st->fill += take;
+        st->received += take;
+        p += take;
+        len -= take;
+        if (st->fill == kStreamStage) {
+            int rc = stream_flush(st);
+            if (rc != DM_OK) return rc;
+        }
+    }
+    return DM_OK;
+}
+
+const char* dm_stream_error(dm_stream* st) { return st ? st->err.c_str() : ""; }
+
+int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_t* nleaves, uint8_t root[32]) {
+    if (!st || !root) return DM_ERR_INVALID;
+    dm_ctx* c = st->c;
+    int rc = DM_OK;
+    do {
+        if (st->received == 0) {
+            rc = DM_ERR_EMPTY;
+            st->err = "Empty data";
+            break;
+        }
+        if (hipSetDevice(c->devs[st->dev].id) != hipSuccess) { rc = DM_ERR_HIP; break; }
+        if ((rc = stream_flush(st)) != DM_OK) break;
+        const uint64_t n = ceil_div(st->received, st->chunk);
+        if ((rc = stream_launch(st, n, st->received - (n - 1) * st->chunk)) != DM_OK) break;
+        if (nleaves) *nleaves = n;
+        // tree over all leaf digests on the context's stream, after every compute stream
+        std::lock_guard<std::mutex> lk(c->mu);
+        Dev& d = c->devs[st->dev];
+        hipStream_t s = d.stream;
+        if ((rc = begin_call(c, d, s)) != DM_OK) break;
+        for (int k = 0; k < kStreamLanes; k++) {
+            hipError_t e = hipStreamWaitEvent(s, st->ev_comp[k], 0);
+            if (e != hipSuccess) { rc = fail(c, DM_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)); break; }
+        }
+        if (rc != DM_OK) break;
+        hipError_t e = d.leaves.ensure(n * 32);
+        if (e != hipSuccess) { rc = fail(c, DM_ERR_NOMEM, "leaf digests: %s", hipGetErrorString(e)); break; }
+        for (uint64_t si = 0; si < st->segs.size() && rc == DM_OK; si++) {
+            const uint64_t l0 = si * st->seg_leaves;
+            if (l0 >= n) break;
+            const uint64_t cnt = std::min(st->seg_leaves, n - l0);
+            e = hipMemcpyAsync(d.leaves.u8() + 32 * l0, st->segs[si]->digests.p, cnt * 32, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) rc = fail(c, DM_ERR_HIP, "digest gather: %s", hipGetErrorString(e));
+        }
+        if (rc != DM_OK) break;
+        if ((rc = finish(c, d, s, d.leaves.u8(), n, true, d.root.u8())) != DM_OK) break;
+        if ((e = hipMemcpyAsync(root, d.root.p, 32, hipMemcpyDeviceToHost, s)) != hipSuccess) {
+            rc = fail(c, DM_ERR_HIP, "root copy: %s", hipGetErrorString(e));
+            break;
+        }
+        if (leaf_out && leaf_cap) {
+            e = hipMemcpyAsync(leaf_out, d.leaves.p, std::min(leaf_cap, n) * 32, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) { rc = fail(c, DM_ERR_HIP, "leaf copy: %s", hipGetErrorString(e)); break; }
+        }
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) rc = fail(c, DM_ERR_HIP, "close sync: %s", hipGetErrorString(e));
+    } while (0);
+    if (rc != DM_OK && !st->err.empty()) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        if (c->err.empty() || rc == DM_ERR_EMPTY) c->err = st->err;
+    }
+    stream_free(st);
+    return rc;
+}
+
+void dm_stream_abort(dm_stream* st) { stream_free(st); }
+
+}  // extern "C"

@@ -155,6 +155,11 @@ class MerkleContext:
         self._check(self._L.dm_fill_synthetic_async(self._h, ctypes.c_void_p(dev_ptr), off, nbytes, seed,
                                                     ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
 
+    # -- streaming -------------------------------------------------------------------------------
+    def open_stream(self, chunk: int) -> "MerkleStream":
+        """Incremental root of one object written in pieces (hash while receiving)."""
+        return MerkleStream(self, chunk)
+
     # -- tuning --------------------------------------------------------------------------------
     LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2, "pair": 3}
 
@@ -181,3 +186,59 @@ class MerkleContext:
         self._check(self._L.dm_timing_summary(self._h, ctypes.byref(n), ctypes.byref(a), ctypes.byref(b),
                                               ctypes.byref(m)), "dm_timing_summary")
         return n.value, a.value, b.value, m.value
+
+
+class MerkleStream:
+    """dm_stream_*: write() pieces of any size, close() -> (leaf digests, root)."""
+
+    def __init__(self, ctx: MerkleContext, chunk: int):
+        self._ctx = ctx
+        self._L = ctx._L
+        h = ctypes.c_void_p()
+        ctx._check(self._L.dm_stream_open(ctx._h, chunk, ctypes.byref(h)), "dm_stream_open")
+        self._h = h
+        self.chunk = chunk
+        self.written = 0
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc == 0:
+            return
+        if rc == DM_ERR_EMPTY:
+            raise DeossMerkleError(rc, "Empty data")
+        detail = (self._L.dm_stream_error(self._h) or b"").decode() if self._h else ""
+        raise DeossMerkleError(rc, f"{what}: {self._L.dm_strerror(rc).decode()}: {detail}")
+
+    def write(self, data) -> None:
+        if isinstance(data, (bytes, bytearray)):
+            buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+            self._check(self._L.dm_stream_write(self._h, buf, len(data)), "dm_stream_write")
+            self.written += len(data)
+        else:   # (address, length) of host memory
+            addr, n = data
+            self._check(self._L.dm_stream_write(self._h, ctypes.c_void_p(addr), n), "dm_stream_write")
+            self.written += n
+
+    def close(self, want_leaves: bool = False, leaf_cap: int = 0) -> Tuple[Optional[bytes], bytes]:
+        cap = leaf_cap if leaf_cap else (-(-self.written // self.chunk) if want_leaves else 0)
+        leaf = ctypes.create_string_buffer(max(32 * cap, 32)) if want_leaves else None
+        n = ctypes.c_uint64()
+        root = ctypes.create_string_buffer(32)
+        h, self._h = self._h, None
+        rc = self._L.dm_stream_close(h, leaf, cap if want_leaves else 0, ctypes.byref(n), root)
+        if rc != 0:
+            if rc == DM_ERR_EMPTY:
+                raise DeossMerkleError(rc, "Empty data")
+            detail = (self._L.dm_last_error(self._ctx._h) or b"").decode()
+            raise DeossMerkleError(rc, f"dm_stream_close: {self._L.dm_strerror(rc).decode()}: {detail}")
+        return (leaf.raw[:32 * min(n.value, cap)] if want_leaves else None), root.raw
+
+    def abort(self) -> None:
+        if self._h:
+            self._L.dm_stream_abort(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.abort()
+        except Exception:
+            pass

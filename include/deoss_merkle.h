@@ -75,6 +75,21 @@ int dm_root_buffer(dm_ctx *ctx, const void *host, uint64_t len, uint64_t chunk,
 int dm_root_batch(dm_ctx *ctx, const void *const *objs, const uint64_t *lens, uint64_t nobj,
                   uint64_t chunk, uint8_t *roots);
 
+/* ---- streaming: hash while the bytes arrive ------------------------------------------------
+ * One object whose bytes are handed over in pieces of any size (e.g. the HTTP upload body as it
+ * is received), split into `chunk`-byte leaves (chunk a multiple of 16).  Whole leaves are hashed
+ * on the GPU while later pieces are still arriving; close pads the last leaf, builds the tree and
+ * frees the stream.  A stream is used by one thread at a time; many streams may share a ctx. */
+typedef struct dm_stream dm_stream;
+int dm_stream_open(dm_ctx *ctx, uint64_t chunk, dm_stream **out);
+int dm_stream_write(dm_stream *st, const void *data, uint64_t len);
+/* Root of everything written; leaf_out (nullable) receives min(n, leaf_cap) x 32 bytes of leaf
+ * digests, *nleaves (nullable) the leaf count n.  No bytes written -> DM_ERR_EMPTY. */
+int dm_stream_close(dm_stream *st, uint8_t *leaf_out, uint64_t leaf_cap, uint64_t *nleaves,
+                    uint8_t root[32]);
+void dm_stream_abort(dm_stream *st);
+const char *dm_stream_error(dm_stream *st);
+
 /* ---- device-resident entry points ------------------------------------------------------- */
 
 /* Root of an object already in HBM on the context's first device (synchronous). */

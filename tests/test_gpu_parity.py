@@ -287,6 +287,56 @@ def test_host_buffer_many_leaves(ctx, oracle_lib, leaf_mode):
     assert root == want
 
 
+# ---------------------------------------------------------------- streaming (hash while receiving)
+@pytest.mark.parametrize("chunk,length", [(64, 10000), (4096, 3 * (1 << 20) + 5), (1 << 20, (9 << 20) + 123),
+                                          (32 << 20, (70 << 20) + 77), (4096, 4096), (16, 1)])
+def test_stream_random_pieces(ctx, oracle_lib, chunk, length):
+    import random
+    rnd = random.Random(length)
+    host = oracle_lib.splitmix_bytes(length, chunk + length)
+    lw, want = oracle_lib.root_buffer(host, chunk)
+    st = ctx.open_stream(chunk)
+    pos = 0
+    while pos < length:
+        n = min(length - pos, rnd.choice([1, 7, 64, 1000, 65536, 1 << 20, 5 << 20]))
+        st.write(host[pos:pos + n])
+        pos += n
+    leaves, root = st.close(want_leaves=True)
+    assert root == want and leaves == lw
+
+
+def test_stream_errors(ctx):
+    from deoss_amd import DeossMerkleError
+    st = ctx.open_stream(64)
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        st.close()
+    with pytest.raises(DeossMerkleError):
+        ctx.open_stream(100)     # not a multiple of 16
+    st = ctx.open_stream(64)
+    st.write(b"abc")
+    st.abort()
+
+
+def test_stream_concurrent_uploads(ctx, oracle_lib):
+    """Several uploads streaming through one context from different threads (gin handlers)."""
+    objs = [oracle_lib.splitmix_bytes(3_000_000 + 4097 * i, 40 + i) for i in range(6)]
+    wants = [oracle_lib.root_buffer(o, 65536)[1] for o in objs]
+    got = [None] * len(objs)
+
+    def up(i):
+        st = ctx.open_stream(65536)
+        for p in range(0, len(objs[i]), 300_001):
+            st.write(objs[i][p:p + 300_001])
+        got[i] = st.close()[1]
+
+    th = [threading.Thread(target=up, args=(i,)) for i in range(len(objs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert got == wants
+
+
 # ---------------------------------------------------------------- concurrency (gin handlers)
 def test_concurrent_callers(ctx, oracle_lib):
     """Several host threads share one context (calls serialise inside) plus private contexts."""
