@@ -295,6 +295,7 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         "config": {"workload": f"{length} B object written in {piece} B pieces, chunk {chunk}",
                    "leaf_kernel": ctx.leaf_kernel_for(min(64, (length + chunk - 1) // chunk))},
         "tail_ms_after_last_write": round(sum(tails) / len(tails) * 1e3, 3),
+        "write_ms": round((tavg - sum(tails) / len(tails)) * 1e3, 3),
         "parity": {"root": root.hex(), "cpu_root": want.hex(), "bit_exact": root == want},
     }
     print(json.dumps(out), flush=True)

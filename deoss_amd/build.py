@@ -12,8 +12,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SRC = os.path.join(HERE, "csrc", "merkle_capi.hip")
-HDRS = [os.path.join(HERE, "csrc", f) for f in ("merkle_kernels.hpp", "sha256_gfx950.hpp")] + [
-    os.path.join(ROOT, "include", "deoss_merkle.h")]
+HDRS = sorted(os.path.join(HERE, "csrc", f) for f in os.listdir(os.path.join(HERE, "csrc"))
+              if f.endswith((".hpp", ".inl", ".h"))) + [os.path.join(ROOT, "include", "deoss_merkle.h")]
 OUT = os.path.join(HERE, "libdeoss_merkle.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = "gfx950"

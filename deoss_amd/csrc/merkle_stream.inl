@@ -11,13 +11,23 @@
 namespace {
 
 constexpr uint64_t kStreamStage = 64ull << 20;   // pinned staging slot
-constexpr int kStreamLanes = 4;                  // concurrent compute streams per object
-constexpr uint64_t kStreamMinLeaves = 64;        // launch when this many whole leaves wait...
-constexpr uint64_t kStreamMinBytes = 1ull << 30; // ...or this many bytes of them
+constexpr int kStreamLanes = 2;                  // concurrent compute streams per object
+// A batch launches once it can fill the chip by itself (32 leaves per CU in the pair kernel) or
+// holds this many bytes: every launch of a long-leaf object then runs ~one leaf-time, and
+// staging copies are not queued behind a stream of small latency-bound launches.
+constexpr uint64_t kStreamLeavesPerCu = 32;
+constexpr uint64_t kStreamMinBytes = 4ull << 30;
 
 struct StreamSeg {
     DevBuf data;      // seg_leaves * chunk bytes
-    DevBuf digests;   // seg_leaves * 32 bytes
+};
+
+// One leaf-kernel launch: its leaves may span segments (table mode), its digests are its own.
+struct StreamBatch {
+    uint64_t first = 0, count = 0;
+    DevBuf tab;       // count x (address, length)
+    DevBuf digests;   // count x 32 bytes
+    PinnedBuf htab;   // host side of tab (kept until the launch has run)
 };
 
 }  // namespace
@@ -28,6 +38,7 @@ struct dm_stream {
     uint64_t chunk = 0;
     uint64_t seg_leaves = 0;
     std::vector<StreamSeg*> segs;
+    std::vector<StreamBatch*> batches;
     PinnedBuf stage[2];
     hipEvent_t ev_stage[2] = {nullptr, nullptr};
     bool busy[2] = {false, false};
@@ -66,46 +77,56 @@ int stream_seg_for(dm_stream* st, uint64_t leaf, StreamSeg** out) {
         StreamSeg* g = new StreamSeg();
         st->segs.push_back(g);
         SHIP(g->data.ensure(st->seg_leaves * st->chunk));
-        SHIP(g->digests.ensure(st->seg_leaves * 32));
     }
     *out = st->segs[si];
     return DM_OK;
 }
 
-// Enqueue hashing of leaves [launched, upto); the leaf upto-1 may be the short last one.
+// Enqueue hashing of leaves [launched, upto) as ONE launch (table mode across segments, so a
+// batch of long leaves runs concurrently, never as a serial chain of per-segment launches); the
+// leaf upto-1 may be the short last one.
 int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
     if (upto <= st->launched) return DM_OK;
+    StreamBatch* bt = new StreamBatch();
+    st->batches.push_back(bt);
+    bt->first = st->launched;
+    bt->count = upto - st->launched;
+    const uint64_t n = bt->count;
+    SHIP(bt->htab.ensure(16 * n));
+    SHIP(bt->tab.ensure(16 * n));
+    SHIP(bt->digests.ensure(32 * n));
+    uint64_t* h = reinterpret_cast<uint64_t*>(bt->htab.p);
+    for (uint64_t j = 0; j < n; j++) {
+        const uint64_t leaf = bt->first + j;
+        StreamSeg* g;
+        int rc = stream_seg_for(st, leaf, &g);
+        if (rc != DM_OK) return rc;
+        h[j] = reinterpret_cast<uint64_t>(g->data.u8() + (leaf % st->seg_leaves) * st->chunk);
+        h[n + j] = (leaf + 1 == upto) ? last_len : st->chunk;
+    }
     SHIP(hipEventRecord(st->ev_copy, st->copy));
     const int k = st->next_comp++ % kStreamLanes;
     hipStream_t s = st->comp[k];
     SHIP(hipStreamWaitEvent(s, st->ev_copy, 0));
-    while (st->launched < upto) {
-        StreamSeg* g;
-        int rc = stream_seg_for(st, st->launched, &g);
-        if (rc != DM_OK) return rc;
-        const uint64_t first = st->launched % st->seg_leaves;
-        const uint64_t n = std::min(upto - st->launched, st->seg_leaves - first);
-        dm::LeafArgs la{};
-        la.base = g->data.u8() + first * st->chunk;
-        la.pitch = st->chunk;
-        la.leaf_len = st->chunk;
-        la.last_len = (st->launched + n == upto) ? last_len : st->chunk;
-        la.nleaves = n;
-        la.byte_end = ~0ull;
-        la.digests = g->digests.u8() + first * 32;
-        const int kind = pick_leaf_kernel(st->c, st->c->devs[st->dev], n);
-        if (kind == DM_LEAF_PAIR)
-            hipLaunchKernelGGL((dm::leaf_kernel_pair<false, true>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
-                               dim3(dm::kLatThreads), 0, s, la);
-        else if (kind == DM_LEAF_LATENCY)
-            hipLaunchKernelGGL((dm::leaf_kernel_lat<false, true>), dim3((uint32_t)ceil_div(n, dm::kLatLeaves)),
-                               dim3(dm::kLatThreads), 0, s, la);
-        else
-            hipLaunchKernelGGL((dm::leaf_kernel<false, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock),
-                               0, s, la);
-        SHIP(hipGetLastError());
-        st->launched += n;
-    }
+    SHIP(hipMemcpyAsync(bt->tab.p, bt->htab.p, 16 * n, hipMemcpyHostToDevice, s));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(bt->tab.p);
+    la.lens = la.addrs + n;
+    la.nleaves = n;
+    la.byte_end = ~0ull;
+    la.digests = bt->digests.u8();
+    const int kind = pick_leaf_kernel(st->c, st->c->devs[st->dev], n);
+    if (kind == DM_LEAF_PAIR)
+        hipLaunchKernelGGL((dm::leaf_kernel_pair<true, true>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
+                           dim3(dm::kLatThreads), 0, s, la);
+    else if (kind == DM_LEAF_LATENCY)
+        hipLaunchKernelGGL((dm::leaf_kernel_lat<true, true>), dim3((uint32_t)ceil_div(n, dm::kLatLeaves)),
+                           dim3(dm::kLatThreads), 0, s, la);
+    else
+        hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock), 0,
+                           s, la);
+    SHIP(hipGetLastError());
+    st->launched = upto;
     SHIP(hipEventRecord(st->ev_comp[k], s));
     return DM_OK;
 }
@@ -134,7 +155,8 @@ int stream_flush(dm_stream* st) {
     st->fill = 0;
     const uint64_t ready = st->on_device / st->chunk;
     const uint64_t pending = ready > st->launched ? ready - st->launched : 0;
-    if (pending >= kStreamMinLeaves || pending * st->chunk >= kStreamMinBytes)
+    const uint64_t fill_leaves = kStreamLeavesPerCu * (uint64_t)st->c->devs[st->dev].cus;
+    if (pending >= fill_leaves || pending * st->chunk >= kStreamMinBytes)
         return stream_launch(st, ready, st->chunk);
     return DM_OK;
 }
@@ -147,8 +169,13 @@ void stream_free(dm_stream* st) {
         if (st->comp[k]) (void)hipStreamSynchronize(st->comp[k]);
     for (StreamSeg* g : st->segs) {
         g->data.release();
-        g->digests.release();
         delete g;
+    }
+    for (StreamBatch* b : st->batches) {
+        b->tab.release();
+        b->digests.release();
+        b->htab.release();
+        delete b;
     }
     st->stage[0].release();
     st->stage[1].release();
@@ -181,7 +208,11 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     do {
         hipError_t e;
         if ((e = hipSetDevice(ctx->devs[0].id)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "hipSetDevice", e); break; }
-        if ((e = hipStreamCreateWithFlags(&st->copy, hipStreamNonBlocking)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "stream", e); break; }
+        // copies on a high-priority stream (its own hardware queue): staging reuse must not wait
+        // behind long leaf kernels
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((e = hipStreamCreateWithPriority(&st->copy, hipStreamNonBlocking, hi)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "stream", e); break; }
         for (int k = 0; k < kStreamLanes && rc == DM_OK; k++) {
             if ((e = hipStreamCreateWithFlags(&st->comp[k], hipStreamNonBlocking)) != hipSuccess ||
                 (e = hipEventCreateWithFlags(&st->ev_comp[k], hipEventDisableTiming)) != hipSuccess)
@@ -261,12 +292,9 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         if (rc != DM_OK) break;
         hipError_t e = d.leaves.ensure(n * 32);
         if (e != hipSuccess) { rc = fail(c, DM_ERR_NOMEM, "leaf digests: %s", hipGetErrorString(e)); break; }
-        for (uint64_t si = 0; si < st->segs.size() && rc == DM_OK; si++) {
-            const uint64_t l0 = si * st->seg_leaves;
-            if (l0 >= n) break;
-            const uint64_t cnt = std::min(st->seg_leaves, n - l0);
-            e = hipMemcpyAsync(d.leaves.u8() + 32 * l0, st->segs[si]->digests.p, cnt * 32, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) rc = fail(c, DM_ERR_HIP, "digest gather: %s", hipGetErrorString(e));
+        for (StreamBatch* b : st->batches) {
+            e = hipMemcpyAsync(d.leaves.u8() + 32 * b->first, b->digests.p, b->count * 32, hipMemcpyDeviceToDevice, s);
+            if (e != hipSuccess) { rc = fail(c, DM_ERR_HIP, "digest gather: %s", hipGetErrorString(e)); break; }
         }
         if (rc != DM_OK) break;
         if ((rc = finish(c, d, s, d.leaves.u8(), n, true, d.root.u8())) != DM_OK) break;
