@@ -1,0 +1,21 @@
+#!/bin/bash
+# Build and run tests/cpp/test_capi_host.cpp against (1) the normal library and (2) a build whose
+# host code runs under AddressSanitizer + UndefinedBehaviorSanitizer.  GPU box only.
+set -e
+cd "$(dirname "$0")/../.."
+out=${1:-/tmp/deoss_hosttests}
+mkdir -p $out
+make -s -C oracle
+INC="-I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__"
+LIBS="-L oracle -loracle_merkle -L /opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,$PWD/oracle:/opt/rocm/lib"
+# (1) plain
+g++ -O2 -std=c++17 $INC tests/cpp/test_capi_host.cpp -L deoss_amd -ldeoss_merkle -Wl,-rpath,$PWD/deoss_amd $LIBS -o $out/test_plain
+$out/test_plain
+# (2) sanitized host code
+hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -I include \
+  -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
+  -o $out/libdeoss_merkle_asan.so deoss_amd/csrc/merkle_capi.hip -L /opt/rocm/lib -lrccl
+g++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $INC tests/cpp/test_capi_host.cpp \
+  -L $out -ldeoss_merkle_asan -Wl,-rpath,$out $LIBS -o $out/test_asan
+ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
+  $out/test_asan

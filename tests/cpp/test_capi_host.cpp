@@ -1,0 +1,177 @@
+// Exercise every C-ABI entry point of libdeoss_merkle (include/deoss_merkle.h) from C++, checked
+// against the CPU oracle (oracle/liboracle_merkle.so, linked as the checker only).  Built twice
+// by tests/cpp/run_host_tests.sh: plain, and with the library's HOST code compiled under
+// AddressSanitizer + UBSan (-Xarch_host -fsanitize=...; device code is not instrumented).
+// Prints PASS and exits 0 when everything matches.
+#include <hip/hip_runtime_api.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "deoss_merkle.h"
+
+extern "C" {
+int or_root_buffer(const void* buf, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32], int nthreads);
+int or_root_chunks(const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out, uint8_t root[32],
+                   int nthreads);
+void or_fill_splitmix(void* dst, uint64_t off, uint64_t nbytes, uint64_t seed);
+}
+
+static int fails = 0;
+#define EXPECT(c)                                                                     \
+    do {                                                                              \
+        if (!(c)) {                                                                   \
+            std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, #c);         \
+            fails++;                                                                  \
+        }                                                                             \
+    } while (0)
+
+static std::vector<uint8_t> bytes(uint64_t n, uint64_t seed) {
+    std::vector<uint8_t> v((n + 7) / 8 * 8 + 8);
+    or_fill_splitmix(v.data(), 0, v.size() - 8, seed);
+    v.resize(n);
+    return v;
+}
+
+static void check_buffer(dm_ctx* c, uint64_t len, uint64_t chunk, uint64_t seed) {
+    auto b = bytes(len, seed);
+    const uint64_t n = (len + chunk - 1) / chunk;
+    std::vector<uint8_t> lw(32 * n), lg(32 * n);
+    uint8_t rw[32], rg[32];
+    EXPECT(or_root_buffer(b.data(), len, chunk, lw.data(), rw, 4) == 0);
+    EXPECT(dm_root_buffer(c, b.data(), len, chunk, lg.data(), rg) == DM_OK);
+    EXPECT(std::memcmp(rw, rg, 32) == 0);
+    EXPECT(lw == lg);
+    // device-resident forms
+    void* dev = nullptr;
+    EXPECT(hipMalloc(&dev, len + 64) == hipSuccess);
+    EXPECT(hipMemcpy(dev, b.data(), len, hipMemcpyHostToDevice) == hipSuccess);
+    uint8_t rd[32];
+    EXPECT(dm_root_device(c, dev, len, chunk, rd) == DM_OK);
+    EXPECT(std::memcmp(rw, rd, 32) == 0);
+    void* droot = nullptr;
+    EXPECT(hipMalloc(&droot, 32) == hipSuccess);
+    EXPECT(dm_root_device_async(c, dev, len, chunk, droot, nullptr, nullptr) == DM_OK);
+    EXPECT(hipDeviceSynchronize() == hipSuccess);
+    EXPECT(hipMemcpy(rd, droot, 32, hipMemcpyDeviceToHost) == hipSuccess);
+    EXPECT(std::memcmp(rw, rd, 32) == 0);
+    // subtree + finish over two halves at a block boundary
+    if (n >= 4) {
+        uint32_t k = 0;
+        while ((2ull << k) * 2 <= n) k++;
+        const uint64_t split = (n / (1ull << k) / 2) * (1ull << k) * chunk;
+        if (split > 0 && split < len) {
+            void* nodes = nullptr;
+            EXPECT(hipMalloc(&nodes, 32 * (n + 2)) == hipSuccess);
+            uint64_t c1 = 0, c2 = 0;
+            EXPECT(dm_subtree_device_async(c, dev, split, chunk, k, nodes, &c1, nullptr) == DM_OK);
+            EXPECT(dm_subtree_device_async(c, (uint8_t*)dev + split, len - split, chunk, k, (uint8_t*)nodes + 32 * c1,
+                                           &c2, nullptr) == DM_OK);
+            EXPECT(dm_finish_device_async(c, nodes, c1 + c2, k == 0, droot, nullptr) == DM_OK);
+            EXPECT(hipDeviceSynchronize() == hipSuccess);
+            EXPECT(hipMemcpy(rd, droot, 32, hipMemcpyDeviceToHost) == hipSuccess);
+            EXPECT(std::memcmp(rw, rd, 32) == 0);
+            (void)hipFree(nodes);
+        }
+    }
+    (void)hipFree(droot);
+    (void)hipFree(dev);
+    // streaming with random piece sizes
+    dm_stream* st = nullptr;
+    if (chunk % 16 == 0) {
+        EXPECT(dm_stream_open(c, chunk, &st) == DM_OK);
+        std::mt19937_64 rng(seed);
+        uint64_t pos = 0;
+        while (pos < len) {
+            uint64_t m = std::min<uint64_t>(len - pos, 1 + rng() % (3u << 20));
+            EXPECT(dm_stream_write(st, b.data() + pos, m) == DM_OK);
+            pos += m;
+        }
+        uint64_t nl = 0;
+        std::vector<uint8_t> ls(32 * n);
+        uint8_t rs[32];
+        EXPECT(dm_stream_close(st, ls.data(), n, &nl, rs) == DM_OK);
+        EXPECT(nl == n && std::memcmp(rw, rs, 32) == 0 && ls == lw);
+    }
+}
+
+int main() {
+    dm_ctx* c = nullptr;
+    int rc = dm_create(&c, nullptr, 0);
+    if (rc != DM_OK) {
+        std::fprintf(stderr, "dm_create: %s\n", dm_strerror(rc));
+        return 1;
+    }
+    // argument errors
+    uint8_t root[32];
+    EXPECT(dm_root_buffer(c, nullptr, 0, 64, nullptr, root) == DM_ERR_EMPTY);
+    EXPECT(std::string(dm_last_error(c)) == "Empty data");
+    EXPECT(dm_root_buffer(c, root, 1, 0, nullptr, root) == DM_ERR_INVALID);
+    EXPECT(dm_root_chunks(c, nullptr, nullptr, 0, nullptr, root) == DM_ERR_EMPTY);
+    EXPECT(dm_set_leaf_kernel(c, 9) == DM_ERR_INVALID);
+    EXPECT(std::string(dm_strerror(DM_ERR_EMPTY)) == "Empty data");
+    dm_stream* bad = nullptr;
+    EXPECT(dm_stream_open(c, 100, &bad) == DM_ERR_INVALID && bad == nullptr);
+    const char* missing[] = {"/nonexistent/deoss/chunk"};
+    EXPECT(dm_new_hash_tree(c, missing, 1, nullptr, root) == DM_ERR_IO);
+    EXPECT(std::string(dm_last_error(c)).find("no such file or directory") != std::string::npos);
+
+    for (int mode : {DM_LEAF_AUTO, DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR}) {
+        EXPECT(dm_set_leaf_kernel(c, mode) == DM_OK);
+        check_buffer(c, 1, 64, 1);
+        check_buffer(c, 100000, 1000, 2);
+        check_buffer(c, (3u << 20) + 5, 4096, 3);
+        check_buffer(c, (5u << 20) + 17, 1u << 20, 4);
+    }
+    EXPECT(dm_set_leaf_kernel(c, DM_LEAF_AUTO) == DM_OK);
+    check_buffer(c, (300ull << 20) + 3, 64ull << 20, 5);   // striped host path
+
+    // chunk list with empty chunks, and batches
+    std::vector<std::vector<uint8_t>> ch;
+    for (int i = 0; i < 37; i++) ch.push_back(bytes((i * 977) % 5000, 100 + i));
+    std::vector<const void*> ptrs;
+    std::vector<uint64_t> lens;
+    for (auto& v : ch) {
+        ptrs.push_back(v.data());
+        lens.push_back(v.size());
+    }
+    uint8_t rw[32], rg[32];
+    std::vector<uint8_t> lw(32 * ch.size()), lg(32 * ch.size());
+    EXPECT(or_root_chunks(ptrs.data(), lens.data(), ch.size(), lw.data(), rw, 1) == 0);
+    EXPECT(dm_root_chunks(c, ptrs.data(), lens.data(), ch.size(), lg.data(), rg) == DM_OK);
+    EXPECT(std::memcmp(rw, rg, 32) == 0 && lw == lg);
+    for (auto& l : lens) l = l ? l : 1;
+    std::vector<std::vector<uint8_t>> objs;
+    for (size_t i = 0; i < ch.size(); i++) objs.push_back(bytes(lens[i] * 13, 500 + i));
+    std::vector<const void*> op;
+    std::vector<uint64_t> ol;
+    for (auto& v : objs) {
+        op.push_back(v.data());
+        ol.push_back(v.size());
+    }
+    std::vector<uint8_t> roots(32 * objs.size());
+    EXPECT(dm_root_batch(c, op.data(), ol.data(), objs.size(), 4096, roots.data()) == DM_OK);
+    for (size_t i = 0; i < objs.size(); i++) {
+        uint8_t r[32];
+        or_root_buffer(objs[i].data(), ol[i], 4096, nullptr, r, 1);
+        EXPECT(std::memcmp(r, roots.data() + 32 * i, 32) == 0);
+    }
+
+    // concurrent callers on one context
+    std::vector<std::thread> th;
+    for (int t = 0; t < 4; t++) th.emplace_back([c, t] { check_buffer(c, 200000 + 1111 * t, 4096, 900 + t); });
+    for (auto& x : th) x.join();
+
+    dm_destroy(c);
+    if (fails) {
+        std::fprintf(stderr, "%d failures\n", fails);
+        return 1;
+    }
+    std::printf("PASS\n");
+    return 0;
+}
