@@ -15,7 +15,8 @@ $out/test_plain
 hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -I include \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
   -o $out/libdeoss_merkle_asan.so deoss_amd/csrc/merkle_capi.hip -L /opt/rocm/lib -lrccl
-g++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $INC tests/cpp/test_capi_host.cpp \
+# same compiler (ROCm clang) as the library's host code, so both use clang's sanitizer runtime
+/opt/rocm/lib/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $INC tests/cpp/test_capi_host.cpp \
   -L $out -ldeoss_merkle_asan -Wl,-rpath,$out $LIBS -o $out/test_asan
 ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
   $out/test_asan
