@@ -44,7 +44,7 @@ def blocks_for(length: int, chunk: int) -> int:
     return leaf_blocks + 2 * nodes
 
 
-LEAF_GRID = {"wide": (256, 256), "latency": (64, 128), "pair": (32, 128)}   # leaves, threads per WG
+LEAF_GRID = {"wide": (256, 256), "latency": (64, 128), "pair": (32, 128), "quad": (8, 128)}   # leaves, threads per WG
 
 
 def load_traffic(kind: str, n_leaves: int):
@@ -85,8 +85,8 @@ def main() -> None:
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
     ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
-    ap.add_argument("--sweep-modes", action="store_true", help="sweep every leaf kernel (wide, latency, pair)")
-    ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair"])
+    ap.add_argument("--sweep-modes", action="store_true", help="sweep every leaf kernel (wide, latency, pair, quad)")
+    ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair", "quad"])
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = CPU exchange (rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
@@ -187,7 +187,8 @@ def main() -> None:
     traffic, traffic_src = load_traffic(kind, n_local)
     kernel_name = {"wide": "leaf_kernel (K1, one lane per leaf)",
                    "latency": "leaf_kernel_lat (K1L, producer/consumer waves)",
-                   "pair": "leaf_kernel_pair (K1P, producer/consumer, rounds on lane pairs)"}[kind]
+                   "pair": "leaf_kernel_pair (K1P, producer/consumer, rounds on lane pairs)",
+                   "quad": "leaf_kernel_quad (K1Q, producer/consumer, rounds spread over 8 lanes)"}[kind]
 
     out = {
         "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling",
@@ -447,7 +448,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     if args.sweep and not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
-        modes = ["wide", "latency", "pair"] if args.sweep_modes else ["auto"]
+        modes = ["wide", "latency", "pair", "quad"] if args.sweep_modes else ["auto"]
         for c, mode in [(int(x), m) for x in args.sweep_chunks.split(",") for m in modes]:
             ctx.set_leaf_kernel(mode)
             reps = 3 if c < (8 << 20) else 2

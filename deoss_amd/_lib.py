@@ -81,6 +81,20 @@ def _declare(L: ctypes.CDLL) -> None:
         f.restype = res
 
 
+def _share_torch_runtime() -> None:
+    """Let PyTorch's HIP runtime load first when PyTorch is installed.
+
+    torch ships its own libamdhip64 with the same soname (libamdhip64.so.7) as /opt/rocm's, so
+    one process gets ONE runtime: whichever is loaded first.  The library then uses torch's
+    (device pointers and hipStream_t handles from torch stay valid in dm_* calls); loaded the
+    other way round, torch.cuda finds a runtime it was not built against and reports no GPU.
+    Outside Python (Go, C++) the library uses /opt/rocm's runtime as linked."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load the HIP library; raises (never falls back) when it is absent."""
     global _lib
@@ -91,6 +105,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
             raise DeossMerkleError(
                 DM_ERR_NODEV,
                 f"{path} not built: run __graft_entry__.build() (hipcc --offload-arch=gfx950)")
+        _share_torch_runtime()
         L = ctypes.CDLL(path)
         _declare(L)
         _lib = L

@@ -246,7 +246,10 @@ int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
 template <bool TABLE, bool ALIGNED>
 void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
     const uint64_t n = la.nleaves;
-    if (kind == DM_LEAF_PAIR)
+    if (kind == DM_LEAF_QUAD)
+        hipLaunchKernelGGL((dm::leaf_kernel_quad<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kQuadLeaves)),
+                           dim3(dm::kLatThreads), 0, s, la);
+    else if (kind == DM_LEAF_PAIR)
         hipLaunchKernelGGL((dm::leaf_kernel_pair<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
                            dim3(dm::kLatThreads), 0, s, la);
     else if (kind == DM_LEAF_LATENCY)
@@ -275,7 +278,8 @@ int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool
     const uint64_t n = la.nleaves;
     const int kind = pick_leaf_kernel(c, d, n);
     const uint32_t D = levels < 0 ? std::max<uint32_t>(1, ceil_log2(n)) : (uint32_t)levels;
-    const uint32_t fuse_max = kind == DM_LEAF_PAIR ? dm::kPairFuseMax
+    const uint32_t fuse_max = kind == DM_LEAF_QUAD ? dm::kQuadFuseMax
+                              : kind == DM_LEAF_PAIR ? dm::kPairFuseMax
                               : kind == DM_LEAF_LATENCY ? dm::kLatFuseMax : dm::kLeafFuseMax;
     const uint32_t L1 = std::min<uint32_t>(fuse_max, D);
     const uint64_t m1 = ceil_shift(n, L1);
@@ -786,7 +790,7 @@ void dm_destroy(dm_ctx* ctx) {
 }
 
 int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
-    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_PAIR) return DM_ERR_INVALID;
+    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_QUAD) return DM_ERR_INVALID;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->leaf_mode = mode;
     return DM_OK;

@@ -504,6 +504,185 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// K1Q: the rounds of one leaf spread over 8 lanes, for the fewest, longest leaves.  In K1P the
+// consumer wave still issues 3 rotations + an xor3 per Sigma; here each of three lanes does one
+// rotation (one v_alignbit with a per-lane shift) and two DPP xors combine them, so every lane of
+// the triple holds Sigma.  Lanes 8c+0..2 (e-triple) hold (e,f,g,h), lanes 8c+4..6 (a-triple)
+// (a,b,c,d), lanes 8c+3 / 8c+7 idle.  Per round, with per-lane constants (e / a):
+//   R  = rotr(X4, s)                        s = 6,11,25 / 2,13,22
+//   S  = R ^ R[q1] ^ R[q2]  (two DPP xors)  Sigma1(e) / Sigma0(a)
+//   F  = bitop3 pair of K1P                 Ch(e,f,g) / Maj(a,b,c)
+//   H' = (X7 ^ N) + V                       h + KW / -d            (N = 0 / ~0, V = KW / 1)
+//   H' += d  on the e-triple                (DPP add from lane+4, bank-masked)
+//   T  = S + F + H'                         e' = T1 + d / Sigma0 + Maj - d
+//   X4' = T (+ T[lane-4] on the a-triple)   e' / T1 + T2           (DPP add, bank-masked)
+// 9 instructions (11 issue slots) per round instead of K1P's 11 (15).  The producer wave gives
+// each of a leaf's 8 lanes its own block (8 consecutive blocks per ring stage, 512 contiguous
+// bytes per leaf per load), so one producer wave keeps up with the faster consumer.
+// LDS: K+W ring [stage][group of 4 rounds][block][leaf] x 16 B (a producer store is 64
+// consecutive uint4; a consumer load is 8 distinct uint4, each broadcast to a leaf's lanes), and
+// a same-shaped region of ones that the a-triple reads instead (its V is the constant 1).
+constexpr int kQuadLeaves = 8;      // leaves per workgroup (8 consumer lanes per leaf)
+constexpr int kQuadBlocks = 8;      // blocks per leaf per ring stage (one producer lane each)
+constexpr int kQuadFuseMax = 3;     // 8 leaves -> 1 node
+
+// One round, hand-scheduled: hipcc re-associates the two DPP xors and cannot fold a bank-masked
+// DPP move into its add, so the round is written out.  H (= X7 ^ N + V, then + d on the e-triple)
+// of the NEXT round is computed in the shadow of this round's add3; its inputs are this round's
+// X6 (next round's X7) and the next round's V.  Wait states: every DPP source VGPR is written at
+// least two instructions earlier (X4 of the rotation by the previous round's last instruction).
+#define DM_QUAD_ROUND_ASM(X4, X5, X6, X7, H, VN, TAIL)                                  \
+    asm volatile("v_alignbit_b32 %[r], %[x4], %[x4], %[sh]\n\t"                         \
+                 "v_bitop3_b32 %[f], %[x4], %[x5], %[msk] bitop3:0x1e\n\t"              \
+                 "v_bitop3_b32 %[f], %[f], %[x6], %[x5] bitop3:0xca\n\t"                \
+                 "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t" \
+                 "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t" \
+                 "v_add3_u32 %[x7], %[s], %[f], %[h]\n\t"                               \
+                 TAIL                                                                   \
+                 "v_add_u32_dpp %[x7], %[x7], %[x7] row_shr:4 row_mask:0xf bank_mask:0xa" \
+                 : [x7] "+v"(X7), [h] "+v"(H), [r] "=&v"(r_), [f] "=&v"(f_), [s] "=&v"(s_) \
+                 : [x4] "v"(X4), [x5] "v"(X5), [x6] "v"(X6), [sh] "v"(sh), [msk] "v"(msk), \
+                   [neg] "v"(neg), [vn] "v"(VN))
+// next round's H from (X6, VN)
+#define DM_QUAD_NEXT_H                                                                  \
+    "v_xad_u32 %[h], %[x6], %[neg], %[vn]\n\t"                                          \
+    "v_add_u32_dpp %[h], %[x6], %[h] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+// last round of a block: the next H depends on the feed-forward, so just wait
+#define DM_QUAD_NO_NEXT "s_nop 1\n\t"
+
+// 64 rounds of one block from the ring (kw: this lane's column, stride kQuadBlocks*kQuadLeaves).
+__device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
+                                                    uint32_t neg) {
+    constexpr int G = kQuadBlocks * kQuadLeaves;
+    uint32_t x4 = x[0], x5 = x[1], x6 = x[2], x7 = x[3];
+    uint32_t r_, f_, s_, h;
+    uint4 q = kw[0];
+    // H of round 0: (x7 ^ N) + V, + d on the e-triple (x7 may have just been written: wait first)
+    asm volatile("s_nop 1\n\t"
+                 "v_xad_u32 %[h], %[x7], %[neg], %[v]\n\t"
+                 "v_add_u32_dpp %[h], %[x7], %[h] row_shl:4 row_mask:0xf bank_mask:0x5"
+                 : [h] "=&v"(h)
+                 : [x7] "v"(x7), [neg] "v"(neg), [v] "v"(q.x));
+#pragma unroll
+    for (int g = 0; g < 16; g++) {
+        uint4 nq = q;
+        if (g + 1 < 16) nq = kw[(g + 1) * G];
+        // register roles rotate: each round's new X4 lands in its X7 register
+        DM_QUAD_ROUND_ASM(x4, x5, x6, x7, h, q.y, DM_QUAD_NEXT_H);
+        DM_QUAD_ROUND_ASM(x7, x4, x5, x6, h, q.z, DM_QUAD_NEXT_H);
+        DM_QUAD_ROUND_ASM(x6, x7, x4, x5, h, q.w, DM_QUAD_NEXT_H);
+        if (g + 1 < 16) {
+            DM_QUAD_ROUND_ASM(x5, x6, x7, x4, h, nq.x, DM_QUAD_NEXT_H);
+        } else {
+            DM_QUAD_ROUND_ASM(x5, x6, x7, x4, h, nq.x, DM_QUAD_NO_NEXT);
+        }
+        q = nq;
+    }
+    x[0] += x4; x[1] += x5; x[2] += x6; x[3] += x7;
+}
+
+template <bool TABLE, bool ALIGNED>
+__global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
+    constexpr int G = kQuadBlocks * kQuadLeaves;              // uint4 per group row
+    // [role: 0 = K+W, 1 = ones][stage][group][block][leaf]
+    __shared__ uint4 ring[2][kLatRing][16][G];
+    __shared__ uint32_t lds_a[kQuadLeaves][8];
+    __shared__ uint32_t lds_b[kQuadLeaves / 2][8];
+    const uint32_t lane = threadIdx.x & 63;
+    const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
+    const uint32_t c = lane >> 3;                             // leaf within the workgroup
+    const uint32_t j = lane & 7;                              // producer: block; consumer: role
+    const uint64_t first = (uint64_t)blockIdx.x * kQuadLeaves;
+    const uint64_t i = first + c;
+    const LeafView v = leaf_view<TABLE>(a, i);
+    const uint64_t NB = wave_max_u64(v.nb);
+    const uint64_t NI = (NB + kQuadBlocks - 1) / kQuadBlocks;
+    {
+        uint4* ones = &ring[1][0][0][0];
+        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * G; t += kLatThreads) ones[t] = make_uint4(1, 1, 1, 1);
+    }
+    __syncthreads();
+    if (producer) {
+        // lane (c, j) schedules blocks j, j+8, j+16, ... of leaf c
+        Blk cur;
+        if (j < v.nb) cur = load_block<ALIGNED>(v.p + 64 * j);
+        for (uint64_t it = 0; it < NI; it++) {
+            const uint64_t b = it * kQuadBlocks + j;
+            if (b < v.nb) {
+                uint32_t w[16];
+                block_words(cur, w);
+                if (b + kQuadBlocks < v.nb) cur = load_block<ALIGNED>(v.p + 64 * (b + kQuadBlocks));
+                uint4* kw = &ring[0][it % kLatRing][0][j * kQuadLeaves + c];
+#pragma unroll
+                for (int q = 0; q < 16; q++) {
+                    uint32_t u[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int t = 4 * q + k;
+                        uint32_t wt;
+                        if (t < 16) {
+                            wt = w[t];
+                        } else {
+                            wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
+                            w[t & 15] = wt;
+                        }
+                        u[k] = kSha256K[t] + wt;
+                    }
+                    kw[q * G] = make_uint4(u[0], u[1], u[2], u[3]);
+                }
+            }
+            __syncthreads();   // stage it full  /  stage it-1 free
+        }
+        __syncthreads();
+    } else {
+        const bool role_a = j >= 4;
+        const uint32_t p = j & 3;
+        const uint32_t sh = role_a ? (p == 0 ? 2 : p == 1 ? 13 : 22) : (p == 0 ? 6 : p == 1 ? 11 : 25);
+        const uint32_t msk = role_a ? 0u : ~0u;
+        const uint32_t neg = role_a ? ~0u : 0u;
+        uint32_t st0[8];
+        if (v.active) load_or_init_state(a, i, st0);
+        else init_state(st0);
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = role_a ? st0[k] : st0[4 + k];
+        const uint4* col = &ring[role_a ? 1 : 0][0][0][c];
+        __syncthreads();
+        for (uint64_t it = 0; it < NI; it++) {
+            const uint4* kw = col + (it % kLatRing) * 16 * G;
+            for (uint32_t k = 0; k < kQuadBlocks; k++) {
+                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw(x, kw + k * kQuadLeaves, sh, msk, neg);
+            }
+            __syncthreads();
+        }
+        // full state on lane 8c: (e,f,g,h) own, (a,b,c,d) from lane 8c+4
+        uint32_t st[8];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            st[k] = __shfl(x[k], (int)(lane + 4), 64);
+            st[4 + k] = x[k];
+        }
+        if (v.active && j == 0) {
+            leaf_epilogue<ALIGNED>(a, i, v, st);
+#pragma unroll
+            for (int k = 0; k < 8; k++) lds_a[c][k] = st[k];
+        }
+    }
+    if (a.fuse_levels == 0) return;
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)((a.nleaves - first) < kQuadLeaves ? (a.nleaves - first) : kQuadLeaves);
+    uint32_t (*res)[8];
+    const uint32_t out_cnt = lds_reduce(lds_a, lds_b, cnt, a.fuse_levels, &res);
+    if (threadIdx.x < out_cnt) {
+        uint32_t o8[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) o8[k] = res[threadIdx.x][k];
+        const uint64_t o = (uint64_t)blockIdx.x * (kQuadLeaves >> a.fuse_levels) + threadIdx.x;
+        store_digest(a.level_out + 32 * o, o8);
+    }
+}
+
 // K2: tree reduce, `levels` (1..9) levels over tiles of 512 input nodes; the first level reads
 // global memory directly, the rest run in LDS.  Output: ceil(m / 2^levels) nodes.
 __global__ __launch_bounds__(kBlock) void reduce_kernel(const uint8_t* in, uint64_t m, uint32_t levels,

@@ -116,15 +116,7 @@ int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
     la.byte_end = ~0ull;
     la.digests = bt->digests.u8();
     const int kind = pick_leaf_kernel(st->c, st->c->devs[st->dev], n);
-    if (kind == DM_LEAF_PAIR)
-        hipLaunchKernelGGL((dm::leaf_kernel_pair<true, true>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
-                           dim3(dm::kLatThreads), 0, s, la);
-    else if (kind == DM_LEAF_LATENCY)
-        hipLaunchKernelGGL((dm::leaf_kernel_lat<true, true>), dim3((uint32_t)ceil_div(n, dm::kLatLeaves)),
-                           dim3(dm::kLatThreads), 0, s, la);
-    else
-        hipLaunchKernelGGL((dm::leaf_kernel<true, true>), dim3((uint32_t)ceil_div(n, dm::kBlock)), dim3(dm::kBlock), 0,
-                           s, la);
+    launch_leaves_t<true, true>(s, la, kind);
     SHIP(hipGetLastError());
     st->launched = upto;
     SHIP(hipEventRecord(st->ev_comp[k], s));

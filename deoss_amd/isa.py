@@ -8,8 +8,9 @@ assembly and counts the instructions of one 64-byte block:
 * ``latency`` (K1L) and ``pair`` (K1P): the consumer loop (16 ds_read_b128 of K+W per block)
   and the producer loop (16 ds_write_b128 per block).
 
-``lanes_per_leaf`` converts wave-instruction counts into lane-slots per leaf-block: K1 runs one
-lane per leaf, K1L two (producer + consumer lane), K1P four (two of each).  Results go to
+``lanes`` converts wave-instruction counts into lane-slots per leaf-block: K1 runs one lane per
+leaf; per leaf-block K1L spends one consumer + one producer lane, K1P two + two, K1Q eight
+consumer lanes + one producer lane (each producer lane schedules its own block).  Results go to
 ``isa_counts.json`` next to this file (it travels with the built library).
 """
 from __future__ import annotations
@@ -26,10 +27,12 @@ COUNTS = os.path.join(HERE, "isa_counts.json")
 # tools/valu_peak.hip (profiles/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
 # the v_add_u32 / v_bitop3_b32 rate.
 SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0}
+# name: (symbol, (consumer lanes, producer lanes) per leaf-block)
 KERNELS = {
-    "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", 1),
-    "latency": ("_ZN2dm15leaf_kernel_latILb0ELb1EEEvNS_8LeafArgsE", 2),
-    "pair": ("_ZN2dm16leaf_kernel_pairILb0ELb1EEEvNS_8LeafArgsE", 4),
+    "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", (1, 0)),
+    "latency": ("_ZN2dm15leaf_kernel_latILb0ELb1EEEvNS_8LeafArgsE", (1, 1)),
+    "pair": ("_ZN2dm16leaf_kernel_pairILb0ELb1EEEvNS_8LeafArgsE", (2, 2)),
+    "quad": ("_ZN2dm16leaf_kernel_quadILb0ELb1EEEvNS_8LeafArgsE", (8, 1)),
 }
 K1_SYMBOL = KERNELS["wide"][0]
 
@@ -125,10 +128,11 @@ def generate() -> dict:
             d["lane_slots_per_leaf_block"] = d["valu_slots"]
         else:
             d = analyse_split(asm, sym)
-            d["lane_slots_per_leaf_block"] = (d["consumer"]["valu_slots"] + d["producer"]["valu_slots"]) * lanes / 2
+            d["lane_slots_per_leaf_block"] = (d["consumer"]["valu_slots"] * lanes[0] +
+                                              d["producer"]["valu_slots"] * lanes[1])
             d["consumer_valu_per_block"] = d["consumer"]["valu"]
         d["kernel"] = sym
-        d["lanes_per_leaf"] = lanes
+        d["lanes_per_leaf_block"] = {"consumer": lanes[0], "producer": lanes[1]}
         res[name] = d
     res["per"] = "one 64-byte block of one leaf"
     with open(COUNTS, "w") as f:

@@ -161,15 +161,16 @@ class MerkleContext:
         return MerkleStream(self, chunk)
 
     # -- tuning --------------------------------------------------------------------------------
-    LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2, "pair": 3}
+    LEAF_KERNELS = {"auto": 0, "wide": 1, "latency": 2, "pair": 3, "quad": 4}
 
     def set_leaf_kernel(self, mode: str) -> None:
         """'auto' | 'wide' (one lane per leaf) | 'latency' (producer/consumer waves) |
-        'pair' (producer/consumer with rounds packed on lane pairs)."""
+        'pair' (producer/consumer with rounds packed on lane pairs) | 'quad' (rounds spread over
+        eight lanes per leaf)."""
         self._check(self._L.dm_set_leaf_kernel(self._h, self.LEAF_KERNELS[mode]), "dm_set_leaf_kernel")
 
     def leaf_kernel_for(self, nleaves: int) -> str:
-        """Leaf kernel ('wide' | 'latency' | 'pair') an object of nleaves uniform chunks runs with."""
+        """Leaf kernel ('wide' | 'latency' | 'pair' | 'quad') an object of nleaves uniform chunks runs with."""
         code = self._L.dm_leaf_kernel_for(self._h, nleaves)
         if code < 0:
             self._check(code, "dm_leaf_kernel_for")

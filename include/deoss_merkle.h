@@ -127,8 +127,9 @@ int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbyte
 /* Leaf-kernel selection for uniform-chunk objects (results are identical in every mode):
  * DM_LEAF_AUTO picks by leaf count; DM_LEAF_WIDE = one lane per leaf (K1, throughput regime);
  * DM_LEAF_LATENCY = producer/consumer waves per 64 leaves (K1L, few long leaves);
- * DM_LEAF_PAIR = K1L with each leaf's rounds packed on two lanes (K1P). */
-enum { DM_LEAF_AUTO = 0, DM_LEAF_WIDE = 1, DM_LEAF_LATENCY = 2, DM_LEAF_PAIR = 3 };
+ * DM_LEAF_PAIR = K1L with each leaf's rounds packed on two lanes (K1P);
+ * DM_LEAF_QUAD = each leaf's rounds spread over eight lanes (K1Q, fewest leaves). */
+enum { DM_LEAF_AUTO = 0, DM_LEAF_WIDE = 1, DM_LEAF_LATENCY = 2, DM_LEAF_PAIR = 3, DM_LEAF_QUAD = 4 };
 int dm_set_leaf_kernel(dm_ctx *ctx, int mode);
 /* The leaf kernel (DM_LEAF_WIDE / _LATENCY / _PAIR) a uniform-chunk object of nleaves leaves
  * runs with under the current setting. */

@@ -114,6 +114,7 @@ int main() {
     EXPECT(dm_root_buffer(c, root, 1, 0, nullptr, root) == DM_ERR_INVALID);
     EXPECT(dm_root_chunks(c, nullptr, nullptr, 0, nullptr, root) == DM_ERR_EMPTY);
     EXPECT(dm_set_leaf_kernel(c, 9) == DM_ERR_INVALID);
+    EXPECT(dm_set_leaf_kernel(c, 5) == DM_ERR_INVALID);
     EXPECT(std::string(dm_strerror(DM_ERR_EMPTY)) == "Empty data");
     dm_stream* bad = nullptr;
     EXPECT(dm_stream_open(c, 100, &bad) == DM_ERR_INVALID && bad == nullptr);
@@ -121,7 +122,7 @@ int main() {
     EXPECT(dm_new_hash_tree(c, missing, 1, nullptr, root) == DM_ERR_IO);
     EXPECT(std::string(dm_last_error(c)).find("no such file or directory") != std::string::npos);
 
-    for (int mode : {DM_LEAF_AUTO, DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR}) {
+    for (int mode : {DM_LEAF_AUTO, DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR, DM_LEAF_QUAD}) {
         EXPECT(dm_set_leaf_kernel(c, mode) == DM_OK);
         check_buffer(c, 1, 64, 1);
         check_buffer(c, 100000, 1000, 2);

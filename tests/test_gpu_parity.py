@@ -89,10 +89,10 @@ def test_new_hash_tree_errors_and_dup(tmp_path):
     assert eq and e is None
 
 
-@pytest.fixture(params=["wide", "latency", "pair"])
+@pytest.fixture(params=["wide", "latency", "pair", "quad"])
 def leaf_mode(request, ctx):
     """Run a test under each leaf kernel: K1 (one lane per leaf), K1L (producer/consumer waves),
-    K1P (producer/consumer, rounds on lane pairs)."""
+    K1P (producer/consumer, rounds on lane pairs), K1Q (rounds over 8 lanes per leaf)."""
     ctx.set_leaf_kernel(request.param)
     yield request.param
     ctx.set_leaf_kernel("auto")

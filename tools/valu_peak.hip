@@ -27,7 +27,11 @@ __device__ __forceinline__ uint32_t op(uint32_t x, uint32_t y, uint32_t z) {
     if constexpr (OP == 0) asm volatile("v_alignbit_b32 %0, %1, %1, %2" : "=v"(r) : "v"(x), "v"(y));
     else if constexpr (OP == 1) asm volatile("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(y), "v"(z));
     else if constexpr (OP == 2) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
-    else asm volatile("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    else if constexpr (OP == 3) asm volatile("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    else if constexpr (OP == 4) asm volatile("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    // DPP add: the nop covers the VALU-write -> DPP-read wait states of a dependent chain
+    else asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf"
+                      : "=v"(r) : "v"(x), "v"(y));
     return r;
 }
 
@@ -88,11 +92,21 @@ int main() {
     double w1_dep_add3 = run<2, 1>(1, 64, iters, out) / 64.0;
     // 8 waves in one workgroup = 2 waves per SIMD, independent chains
     double w8_ind = run<0, 8>(1, 512, iters, out) / 512.0;
+    double xad = run<4, 8>(cus * 4, 256, iters, out);
+    double w1_dep_add = run<3, 1>(1, 64, iters, out) / 64.0;
+    double w1_dep_bitop3 = run<1, 1>(1, 64, iters, out) / 64.0;
+    double w1_dep_xad = run<4, 1>(1, 64, iters, out) / 64.0;
+    double w1_dep_dpp = run<5, 1>(1, 64, iters, out) / 64.0;
+    double w1_ind_add = run<3, 8>(1, 64, iters, out) / 64.0;
     printf("{\"cus\": %d, \"clock_hz_nominal\": %.0f, \"alignbit_lane_ops_s_16w\": %.4e, \"alignbit_lane_ops_s_8w\": %.4e, "
            "\"bitop3_lane_ops_s\": %.4e, \"add3_lane_ops_s\": %.4e, \"add_lane_ops_s\": %.4e, "
            "\"one_wave_indep_cycles_per_inst\": %.3f, \"one_wave_dep_cycles_per_inst\": %.3f, "
-           "\"one_wave_dep_add3_cycles_per_inst\": %.3f, \"two_waves_per_simd_cycles_per_inst_per_wave\": %.3f}\n",
-           cus, clk, al, al8, b3, ad3, ad, clk / w1_ind, clk / w1_dep, clk / w1_dep_add3, clk / w8_ind);
+           "\"one_wave_dep_add3_cycles_per_inst\": %.3f, \"two_waves_per_simd_cycles_per_inst_per_wave\": %.3f, "
+           "\"xad_lane_ops_s\": %.4e, \"one_wave_dep_add_cycles_per_inst\": %.3f, "
+           "\"one_wave_dep_bitop3_cycles_per_inst\": %.3f, \"one_wave_dep_xad_cycles_per_inst\": %.3f, "
+           "\"one_wave_dep_nop_dpp_add_cycles_per_pair\": %.3f, \"one_wave_indep_add_cycles_per_inst\": %.3f}\n",
+           cus, clk, al, al8, b3, ad3, ad, clk / w1_ind, clk / w1_dep, clk / w1_dep_add3, clk / w8_ind, xad,
+           clk / w1_dep_add, clk / w1_dep_bitop3, clk / w1_dep_xad, clk / w1_dep_dpp, clk / w1_ind_add);
     CHK(hipFree(out));
     return 0;
 }
