@@ -230,14 +230,16 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 
 // Hash the leaves described by `la` (uniform or table mode) and reduce `levels` levels
 // (levels < 0: to the root, >= 1 level).  Nodes go to dst; *nout gets their count.
-// Leaf-kernel choice for a uniform-chunk object of n leaves: the producer/consumer latency
-// kernel (K1L) while the leaves cannot fill the chip, the one-lane-per-leaf kernel (K1) after.
-// Returns DM_LEAF_WIDE, DM_LEAF_LATENCY or DM_LEAF_PAIR.
-// Measured (profiles/r01_bench_modes.log, r01_crossover.log): the latency kernels win while
-// every workgroup gets a CU of its own (one consumer wave per SIMD); past that, one lane per
-// leaf with >= 2 waves per SIMD wins.
+// Leaf-kernel choice for a uniform-chunk object of n leaves: the more lanes a kernel spends per
+// leaf, the shorter each leaf's serial chain, as long as its workgroups fit the chip at once.
+// Returns DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR or DM_LEAF_QUAD.
+// Measured on MI355X (profiles/r01_crossover_quad.log, 8 GiB object): K1Q wins up to 4,096
+// leaves (two 64 KiB-LDS workgroups per CU, each consumer wave on its own SIMD), K1P up to
+// 8,192 (one workgroup per CU), K1L up to 16,384; past that one lane per leaf with >= 2 waves
+// per SIMD wins.
 int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
     if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
+    if (ceil_div(n, dm::kQuadLeaves) <= 2 * (uint64_t)d.cus) return DM_LEAF_QUAD;
     if (ceil_div(n, dm::kPairLeaves) <= (uint64_t)d.cus) return DM_LEAF_PAIR;
     if (ceil_div(n, dm::kLatLeaves) <= (uint64_t)d.cus) return DM_LEAF_LATENCY;
     return DM_LEAF_WIDE;
@@ -260,7 +262,7 @@ void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
                            0, s, la);
 }
 
-// Launch the chosen leaf kernel (K1 / K1L / K1P) over la's leaves.
+// Launch the chosen leaf kernel (K1 / K1L / K1P / K1Q) over la's leaves.
 int launch_leaves(dm_ctx* c, hipStream_t s, const dm::LeafArgs& la, bool table, bool aligned, int kind) {
     if (table) {
         if (aligned) launch_leaves_t<true, true>(s, la, kind);

@@ -52,7 +52,6 @@ struct dm_stream {
     uint64_t received = 0;   // bytes handed to dm_stream_write
     uint64_t on_device = 0;  // bytes whose H2D is enqueued
     uint64_t launched = 0;   // leaves whose hashing is enqueued
-    int kind = DM_LEAF_PAIR;
     std::string err;
 };
 

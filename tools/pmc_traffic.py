@@ -20,6 +20,8 @@ KERNEL = "leaf_kernel"
 
 
 def kind(name: str) -> str:
+    if "leaf_kernel_quad" in name:
+        return "quad"
     if "leaf_kernel_pair" in name:
         return "pair"
     if "leaf_kernel_lat" in name:
