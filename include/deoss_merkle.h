@@ -131,7 +131,7 @@ int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbyte
  * DM_LEAF_QUAD = each leaf's rounds spread over eight lanes (K1Q, fewest leaves). */
 enum { DM_LEAF_AUTO = 0, DM_LEAF_WIDE = 1, DM_LEAF_LATENCY = 2, DM_LEAF_PAIR = 3, DM_LEAF_QUAD = 4 };
 int dm_set_leaf_kernel(dm_ctx *ctx, int mode);
-/* The leaf kernel (DM_LEAF_WIDE / _LATENCY / _PAIR) a uniform-chunk object of nleaves leaves
+/* The leaf kernel (DM_LEAF_WIDE / _LATENCY / _PAIR / _QUAD) a uniform-chunk object of nleaves leaves
  * runs with under the current setting. */
 int dm_leaf_kernel_for(dm_ctx *ctx, uint64_t nleaves);
 
