@@ -77,11 +77,12 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
-    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload"],
+    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
                          "upload: one object fed in pieces through dm_stream (hash while receiving)")
     ap.add_argument("--piece-kib", type=int, default=1024, help="upload: bytes per dm_stream_write (KiB)")
+    ap.add_argument("--segment-mib", type=int, default=32, help="rs: segment bytes (chain.SegmentSize)")
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
     ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
@@ -115,6 +116,8 @@ def main() -> None:
 
     if args.workload == "upload":
         return run_upload(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "rs":
+        return run_rs(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload != "object":
         return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
     per_gpu = int(args.object_gib * (1 << 30))
@@ -299,6 +302,118 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         "write_ms": round((tavg - sum(tails) / len(tails)) * 1e3, 3),
         "parity": {"root": root.hex(), "cpu_root": want.hex(), "bit_exact": root == want},
     }
+    print(json.dumps(out), flush=True)
+
+
+def load_rs_traffic(key: str):
+    """PMC HBM bytes per rs_code_kernel launch (profiles/rs_traffic.json, tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "rs_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    e = d.get("by_kernel_grid", {}).get(key)
+    if not e:
+        return None, None
+    return e["hbm_bytes_per_launch"], f"profiles/rs_traffic.json[{key}] <- " + d.get("source", "")
+
+
+def run_rs(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #3: Reed-Solomon 4 + 8 fragment coding (cess-go-sdk via klauspost/reedsolomon, go.mod:65)
+    of device-resident segments.  One step = every segment of this rank coded into 8 parity
+    fragments by one rs_code_kernel launch.  Weak scaling, no exchange (segments are independent)."""
+    from deoss_amd import MerkleContext
+    from deoss_amd.reedsolomon import New
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    seg = args.segment_mib << 20
+    shard = seg // 4
+    nseg = max(1, int(args.object_gib * (1 << 30)) // seg)
+    ctx = MerkleContext(devices=[dev_index])
+    enc = New(ctx, 4, 8)
+    data = torch.empty(nseg * seg, dtype=torch.uint8, device=device)
+    parity = torch.empty(nseg * 2 * seg, dtype=torch.uint8, device=device)
+    sptr = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(data.data_ptr(), 0, nseg * seg, SEED + 0x100 * (rank + 1), sptr)
+
+    def step():
+        enc.encode_device_async(data.data_ptr(), seg, parity.data_ptr(), 2 * seg, shard, nseg, sptr)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    n, k_sum, _, _ = ctx.timing_summary()
+    ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # parity: first and last segment vs the CPU restatement
+    orc = Oracle()
+    checked, ok = [], True
+    for s_i in sorted({0, nseg - 1}):
+        d = data[s_i * seg:(s_i + 1) * seg].cpu().numpy()
+        want = orc.rs_encode([d[j * shard:(j + 1) * shard].tobytes() for j in range(4)], 8,
+                             nthreads=min(16, os.cpu_count() or 1))
+        got = parity[s_i * 2 * seg:(s_i + 1) * 2 * seg].cpu().numpy()
+        same = all(got[i * shard:(i + 1) * shard].tobytes() == want[i] for i in range(8))
+        checked.append(s_i)
+        ok = ok and same
+    if rank != 0:
+        return
+    total = nseg * seg * world
+    k_avg_ms = k_sum / max(n, 1)
+    alg = 3 * nseg * seg                 # read 4 data shards + write 8 parity shards, per launch
+    achieved = alg / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+    grid_key = f"rs:{nseg}x{seg}"
+    traffic, traffic_src = load_rs_traffic(grid_key)
+    out = {
+        "metric": "device-resident GiB/s of segment data Reed-Solomon coded (4 data + 8 parity fragments)",
+        "value": round(total * args.steps / elapsed / (1 << 30), 4), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8 (GF(2^8))",
+        "data": "synthetic splitmix64 segments generated in HBM",
+        "config": {"workload": f"{nseg} segments x {seg} B per GPU -> 4 + 8 fragments of {shard} B "
+                               "(klauspost/reedsolomon New(4, 8) as cess-go-sdk uses it)",
+                   "segments_per_gpu": nseg, "segment_bytes": seg, "parallelism": f"{world} x independent"},
+        "roofline": {"bound": "hbm", "kernel": "rs_code_kernel<4> (LDS table lookup per input byte)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel_avg_ms": round(k_avg_ms, 4), "launches": n, "algorithmic_bytes_per_launch": alg},
+        "parity": {"segments_checked": checked, "bit_exact": ok},
+    }
+    if world == 1 and not args.no_cpu:
+        sample = min(nseg, 8)
+        d = data[:sample * seg].cpu().numpy()
+        import ctypes
+        buf = d.ctypes.data
+        outs = [ctypes.create_string_buffer(shard) for _ in range(8)]
+        pp = [ctypes.addressof(b) for b in outs]
+        res = {}
+        for threads in (1, min(16, os.cpu_count() or 1)):
+            t0 = time.perf_counter()
+            for s_i in range(sample):
+                orc.rs_encode_ptrs(4, 8, [buf + s_i * seg + j * shard for j in range(4)], pp, shard, threads)
+            res[threads] = sample * seg / (time.perf_counter() - t0) / (1 << 30)
+        out["cpu_baseline"] = {"value": round(res[1], 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                               "sample": f"{sample} segments x {seg} B of the same data, scalar table-driven "
+                                         "GF(2^8) encode (oracle/rs_oracle.c, stands in for klauspost's Go path)",
+                               "parallel": {"value": round(res[max(res)], 4), "cores": max(res)}}
     print(json.dumps(out), flush=True)
 
 

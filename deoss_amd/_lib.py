@@ -32,6 +32,8 @@ EXPORTS = (
     "dm_set_timing", "dm_stream_open", "dm_stream_write", "dm_stream_close", "dm_stream_abort",
     "dm_stream_error",
     "dm_timing_summary",
+    "dm_rs_create", "dm_rs_destroy", "dm_rs_matrix", "dm_rs_encode", "dm_rs_encode_buffer", "dm_rs_reconstruct",
+    "dm_rs_verify", "dm_rs_encode_device_async", "dm_rs_reconstruct_device_async",
 )
 
 
@@ -74,6 +76,15 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_set_timing": ([vp, i32], i32),
         "dm_timing_summary": ([vp, pu64, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                ctypes.POINTER(ctypes.c_double)], i32),
+        "dm_rs_create": ([vp, i32, i32, ctypes.POINTER(vp)], i32),
+        "dm_rs_destroy": ([vp], None),
+        "dm_rs_matrix": ([vp, vp], i32),
+        "dm_rs_encode": ([vp, pvp, pvp, u64], i32),
+        "dm_rs_encode_buffer": ([vp, vp, u64, vp, pu64], i32),
+        "dm_rs_reconstruct": ([vp, pvp, vp, u64], i32),
+        "dm_rs_verify": ([vp, pvp, u64, ctypes.POINTER(i32)], i32),
+        "dm_rs_encode_device_async": ([vp, vp, u64, vp, u64, u64, u64, vp], i32),
+        "dm_rs_reconstruct_device_async": ([vp, pvp, vp, u64, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -1017,3 +1017,4 @@ int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t*
 
 // Streaming (incremental) roots: dm_stream_* (shares the helpers above).
 #include "merkle_stream.inl"
+#include "rs_capi.inl"

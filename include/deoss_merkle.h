@@ -122,6 +122,38 @@ int dm_root_batch_device_async(dm_ctx *ctx, const void *const *dev_objs, const u
 int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbytes, uint64_t seed,
                             void *stream);
 
+/* ---- Reed-Solomon fragment coding ------------------------------------------
+ * The stage after hashing on DeOSS's upload path: cess-go-sdk codes every 32 MiB segment into
+ * chain.DataShards = 4 data + chain.ParShards = 8 parity fragments (node/tracker.go:250,369,
+ * node/fileHandler.go:250) with github.com/klauspost/reedsolomon v1.12.4 (go.mod:65).  These
+ * entry points replace that Encoder (default options: GF(2^8) mod 0x11d, Vandermonde-derived
+ * systematic matrix).  Coding runs on the GPU (rs_code_kernel); results are byte-identical to
+ * the restated algorithm (oracle/rs_oracle.c). */
+typedef struct dm_rs dm_rs;
+/* reedsolomon.New(data_shards, parity_shards): 1 <= data <= 8, 1 <= parity <= 8. */
+int dm_rs_create(dm_ctx *ctx, int data_shards, int parity_shards, dm_rs **out);
+void dm_rs_destroy(dm_rs *rs);
+/* The (data + parity) x data encoding matrix, row-major (top data rows = identity). */
+int dm_rs_matrix(dm_rs *rs, uint8_t *out);
+/* Encoder.Encode over host shards: data[j] (j < data) -> parity[i] (i < parity), shard bytes each. */
+int dm_rs_encode(dm_rs *rs, const void *const *data, void *const *parity, uint64_t shard);
+/* Encoder.Split + Encode of one segment: len bytes -> (data + parity) shards of *per_shard =
+ * ceil(len / data) bytes, written back to back to out (the last data shard zero-padded). */
+int dm_rs_encode_buffer(dm_rs *rs, const void *host, uint64_t len, void *out, uint64_t *per_shard);
+/* Encoder.Reconstruct over host shards: rebuilds every shard with present[i] == 0 in place
+ * (needs >= data present; fewer -> DM_ERR_INVALID "too few shards"). */
+int dm_rs_reconstruct(dm_rs *rs, void *const *shards, const uint8_t *present, uint64_t shard);
+/* Encoder.Verify: *ok = 1 when the parity shards match the data shards. */
+int dm_rs_verify(dm_rs *rs, const void *const *shards, uint64_t shard, int *ok);
+/* Device-resident segments (the measured path): segment s has data shard j at
+ * data + s*data_stride + j*shard and gets parity shard i at parity + s*parity_stride + i*shard.
+ * shard, strides and pointers 16-byte aligned; runs on `stream` (NULL = null stream). */
+int dm_rs_encode_device_async(dm_rs *rs, const void *data, uint64_t data_stride, void *parity,
+                              uint64_t parity_stride, uint64_t shard, uint64_t nseg, void *stream);
+/* Reconstruct with device shards (16-byte aligned, shard % 16 == 0), in place, on `stream`. */
+int dm_rs_reconstruct_device_async(dm_rs *rs, void *const *shards, const uint8_t *present, uint64_t shard,
+                                   void *stream);
+
 /* ---- tuning ------------------------------------------------------------------------------ */
 
 /* Leaf-kernel selection for uniform-chunk objects (results are identical in every mode):

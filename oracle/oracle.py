@@ -18,6 +18,13 @@ Reference semantics followed (paths relative to the reference repo):
 * ``cbergoon/merkletree v0.2.0`` (``go.mod:10``; not vendored, restated) -- odd leaf count
   duplicates the last leaf; each level pairs (i, i+1) or (i, i) for a trailing odd node;
   node = SHA-256(left || right); stops at one node, after at least one level.
+
+Reed-Solomon fragment coding (``py_rs_*`` and ``Oracle.rs_*`` over ``oracle/rs_oracle.c``):
+``klauspost/reedsolomon v1.12.4`` (``go.mod:65``; not vendored, restated -- parity unpinned)
+``New(4, 8)`` as the cess-go-sdk uses it for chain.DataShards / chain.ParShards
+(``node/tracker.go:250,369``): GF(2^8) mod x^8+x^4+x^3+x^2+1, Vandermonde matrix times the
+inverse of its top square, parity = matrix rows x data shards.  The Python restatement below
+multiplies bitwise (no log tables) so the two restatements share no tables.
 """
 from __future__ import annotations
 
@@ -104,8 +111,100 @@ def splitmix64_bytes(nbytes: int, seed: int, off: int = 0) -> bytes:
     return z.astype("<u8").tobytes()[:nbytes]
 
 
+def py_gf_mul(a: int, b: int) -> int:
+    """GF(2^8) product, polynomial 0x11d, shift-and-add (klauspost galois.go restated)."""
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        a <<= 1
+        if a & 0x100:
+            a ^= 0x11D
+        b >>= 1
+    return r
+
+
+def py_gf_pow(a: int, n: int) -> int:
+    r = 1
+    for _ in range(n):
+        r = py_gf_mul(r, a)
+    return r
+
+
+def py_gf_inverse(m: List[List[int]]) -> List[List[int]]:
+    k = len(m)
+    w = [list(row) + [int(i == j) for j in range(k)] for i, row in enumerate(m)]
+    for c in range(k):
+        p = next(r for r in range(c, k) if w[r][c])
+        w[c], w[p] = w[p], w[c]
+        inv = next(x for x in range(1, 256) if py_gf_mul(w[c][c], x) == 1)
+        w[c] = [py_gf_mul(v, inv) for v in w[c]]
+        for r in range(k):
+            if r != c and w[r][c]:
+                f = w[r][c]
+                w[r] = [v ^ py_gf_mul(f, u) for v, u in zip(w[r], w[c])]
+    return [row[k:] for row in w]
+
+
+def py_rs_matrix(data: int, total: int) -> List[List[int]]:
+    """klauspost buildMatrix: vandermonde(total, data) x inverse(top data x data square)."""
+    vm = [[py_gf_pow(r, c) for c in range(data)] for r in range(total)]
+    inv = py_gf_inverse(vm[:data])
+    out = []
+    for r in range(total):
+        row = []
+        for c in range(data):
+            acc = 0
+            for t in range(data):
+                acc ^= py_gf_mul(vm[r][t], inv[t][c])
+            row.append(acc)
+        out.append(row)
+    return out
+
+
+def _mul_table():
+    import numpy as np
+    t = np.zeros((256, 256), dtype=np.uint8)
+    for a in range(256):
+        for b in range(256):
+            t[a, b] = py_gf_mul(a, b)
+    return t
+
+
+_MUL = None
+
+
+def py_rs_code(rows: List[List[int]], inputs: Sequence[bytes]) -> List[bytes]:
+    """out[i] = sum_j rows[i][j] * inputs[j] over GF(2^8), bytewise (numpy)."""
+    import numpy as np
+    global _MUL
+    if _MUL is None:
+        _MUL = _mul_table()
+    ins = [np.frombuffer(bytes(x), dtype=np.uint8) for x in inputs]
+    outs = []
+    for row in rows:
+        acc = np.zeros(len(ins[0]), dtype=np.uint8)
+        for c, x in zip(row, ins):
+            acc ^= _MUL[c][x]
+        outs.append(acc.tobytes())
+    return outs
+
+
+def py_rs_split(buf: bytes, data: int) -> List[bytes]:
+    """klauspost Split: perShard = ceil(len / data), the tail zero-padded."""
+    per = (len(buf) + data - 1) // data
+    b = bytes(buf) + bytes(per * data - len(buf))
+    return [b[i * per:(i + 1) * per] for i in range(data)]
+
+
+def py_rs_encode(data_shards: Sequence[bytes], parity: int) -> List[bytes]:
+    k = len(data_shards)
+    m = py_rs_matrix(k, k + parity)
+    return py_rs_code(m[k:], data_shards)
+
+
 class Oracle:
-    """ctypes binding of oracle/merkle_oracle.c."""
+    """ctypes binding of oracle/merkle_oracle.c and oracle/rs_oracle.c."""
 
     def __init__(self, path: str = LIB_PATH):
         if not os.path.exists(path):
@@ -119,6 +218,11 @@ class Oracle:
         L.or_root_buffer.argtypes = [vp, u64, u64, vp, vp, ctypes.c_int]
         L.or_fill_splitmix.argtypes = [vp, u64, u64, u64]
         L.or_set_backend.argtypes = [ctypes.c_int]
+        L.or_rs_matrix.argtypes = [ctypes.c_int, ctypes.c_int, vp]
+        L.or_rs_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                   ctypes.c_size_t, ctypes.c_int]
+        L.or_rs_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), vp, ctypes.c_size_t,
+                                        ctypes.c_int]
         self.L = L
 
     def backend(self) -> str:
@@ -181,3 +285,39 @@ class Oracle:
         b = ctypes.create_string_buffer(max(n8, 8))
         self.fill_splitmix_ptr(ctypes.addressof(b), off, n8, seed)
         return b.raw[:nbytes]
+
+    # -- Reed-Solomon (oracle/rs_oracle.c) ----------------------------------------------------
+    def rs_matrix(self, data: int, total: int) -> List[List[int]]:
+        out = ctypes.create_string_buffer(total * data)
+        if self.L.or_rs_matrix(data, total, out) != 0:
+            raise ValueError("invalid shard counts")
+        return [list(out.raw[r * data:(r + 1) * data]) for r in range(total)]
+
+    def rs_encode_ptrs(self, data: int, parity: int, dptrs: Sequence[int], pptrs: Sequence[int], shard: int,
+                       nthreads: int = 1) -> None:
+        d = (ctypes.c_void_p * data)(*dptrs)
+        p = (ctypes.c_void_p * parity)(*pptrs)
+        if self.L.or_rs_encode(data, parity, d, p, shard, nthreads) != 0:
+            raise ValueError("or_rs_encode failed")
+
+    def rs_encode(self, data_shards: Sequence[bytes], parity: int, nthreads: int = 1) -> List[bytes]:
+        k, n = len(data_shards), len(data_shards[0])
+        ins = [ctypes.create_string_buffer(bytes(x), max(n, 1)) for x in data_shards]
+        outs = [ctypes.create_string_buffer(max(n, 1)) for _ in range(parity)]
+        self.rs_encode_ptrs(k, parity, [ctypes.addressof(b) for b in ins], [ctypes.addressof(b) for b in outs],
+                            n, nthreads)
+        return [b.raw[:n] for b in outs]
+
+    def rs_reconstruct(self, data: int, parity: int, shards: Sequence[Optional[bytes]], shard: int) -> List[bytes]:
+        """Rebuild the shards given as None (klauspost Reconstruct semantics)."""
+        total = data + parity
+        bufs = [ctypes.create_string_buffer(bytes(x) if x is not None else bytes(shard), max(shard, 1))
+                for x in shards]
+        present = bytes(int(x is not None) for x in shards)
+        ptrs = (ctypes.c_void_p * total)(*[ctypes.addressof(b) for b in bufs])
+        rc = self.L.or_rs_reconstruct(data, parity, ptrs, present, shard, 1)
+        if rc == -2:
+            raise ValueError("too few shards")
+        if rc != 0:
+            raise ValueError("or_rs_reconstruct failed")
+        return [b.raw[:shard] for b in bufs]
