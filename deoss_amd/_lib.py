@@ -12,7 +12,8 @@ import threading
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "libdeoss_merkle.so"
-LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
+# DEOSS_MERKLE_LIB: load another build of the same library (a tuning variant, a sanitizer build)
+LIB_PATH = os.environ.get("DEOSS_MERKLE_LIB") or os.path.join(PKG_DIR, LIB_NAME)
 
 DM_OK = 0
 DM_ERR_EMPTY = -1

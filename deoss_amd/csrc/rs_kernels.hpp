@@ -46,9 +46,43 @@ __device__ __forceinline__ void transpose4(uint32_t a, uint32_t b, uint32_t c, u
     o[3] = __builtin_amdgcn_perm(cd_hi, ab_hi, 0x07060302u);
 }
 
+#ifndef DM_RS_NT_STORE
+#define DM_RS_NT_STORE 1
+#endif
+#ifndef DM_RS_NT_LOAD
+#define DM_RS_NT_LOAD 0
+#endif
+#ifndef DM_RS_WAVES
+#define DM_RS_WAVES 0
+#endif
+
+typedef unsigned int rs_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 rs_load(const uint8_t* p) {
+#if DM_RS_NT_LOAD
+    const rs_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rs_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
+__device__ __forceinline__ void rs_store(uint8_t* p, uint4 v) {
+#if DM_RS_NT_STORE
+    const rs_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<rs_u32x4*>(p));
+#else
+    *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+
 // Grid: x strides over a segment's 16-byte units, y over segments (no 64-bit division).
 template <int NIN>
-__global__ __launch_bounds__(kRsThreads) void rs_code_kernel(RsArgs a) {
+__global__ __launch_bounds__(kRsThreads)
+#if DM_RS_WAVES
+__attribute__((amdgpu_waves_per_eu(DM_RS_WAVES)))
+#endif
+void rs_code_kernel(RsArgs a) {
     __shared__ uint2 tab[NIN * 256];
     for (uint32_t t = threadIdx.x; t < NIN * 256; t += kRsThreads) tab[t] = a.table[t];
     __syncthreads();
@@ -56,12 +90,22 @@ __global__ __launch_bounds__(kRsThreads) void rs_code_kernel(RsArgs a) {
     for (uint64_t seg = blockIdx.y; seg < a.nseg; seg += gridDim.y) {
         const uint64_t ib = seg * a.in_seg_stride;
         const uint64_t ob = seg * a.out_seg_stride;
-        for (uint64_t u = (uint64_t)blockIdx.x * kRsThreads + threadIdx.x; u < a.units_per_seg; u += ustride) {
+        uint64_t u = (uint64_t)blockIdx.x * kRsThreads + threadIdx.x;
+        // register double buffer: the next unit's loads are in flight while this one is coded
+        uint4 nx[NIN];
+        if (u < a.units_per_seg) {
+#pragma unroll
+            for (int j = 0; j < NIN; j++) nx[j] = rs_load(a.in[j] + ib + u * 16);
+        }
+        for (; u < a.units_per_seg; u += ustride) {
             const uint64_t off = u * 16;
             uint4 x[NIN];
 #pragma unroll
-            for (int j = 0; j < NIN; j++)
-                x[j] = *reinterpret_cast<const uint4*>(a.in[j] + ib + off);
+            for (int j = 0; j < NIN; j++) x[j] = nx[j];
+            if (u + ustride < a.units_per_seg) {
+#pragma unroll
+                for (int j = 0; j < NIN; j++) nx[j] = rs_load(a.in[j] + ib + off + ustride * 16);
+            }
             uint2 acc[16];
 #pragma unroll
             for (int p = 0; p < 16; p++) acc[p] = make_uint2(0, 0);
@@ -89,12 +133,11 @@ __global__ __launch_bounds__(kRsThreads) void rs_code_kernel(RsArgs a) {
 #pragma unroll
             for (int i = 0; i < 4; i++)
                 if (i < (int)a.nout)
-                    *reinterpret_cast<uint4*>(a.out[i] + ob + off) = make_uint4(lo[0][i], lo[1][i], lo[2][i], lo[3][i]);
+                    rs_store(a.out[i] + ob + off, make_uint4(lo[0][i], lo[1][i], lo[2][i], lo[3][i]));
 #pragma unroll
             for (int i = 0; i < 4; i++)
                 if (i + 4 < (int)a.nout)
-                    *reinterpret_cast<uint4*>(a.out[i + 4] + ob + off) =
-                        make_uint4(hi[0][i], hi[1][i], hi[2][i], hi[3][i]);
+                    rs_store(a.out[i + 4] + ob + off, make_uint4(hi[0][i], hi[1][i], hi[2][i], hi[3][i]));
         }
     }
 }

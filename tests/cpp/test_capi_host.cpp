@@ -20,6 +20,8 @@ int or_root_buffer(const void* buf, uint64_t len, uint64_t chunk, uint8_t* leaf_
 int or_root_chunks(const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out, uint8_t root[32],
                    int nthreads);
 void or_fill_splitmix(void* dst, uint64_t off, uint64_t nbytes, uint64_t seed);
+int or_rs_encode(int data, int parity, const uint8_t* const* dshards, uint8_t* const* pshards, size_t shard,
+                 int nthreads);
 }
 
 static int fails = 0;
@@ -161,6 +163,94 @@ int main() {
         uint8_t r[32];
         or_root_buffer(objs[i].data(), ol[i], 4096, nullptr, r, 1);
         EXPECT(std::memcmp(r, roots.data() + 32 * i, 32) == 0);
+    }
+
+    // Reed-Solomon 4 + 8: host encode / reconstruct / verify / split, device encode, vs the oracle
+    {
+        dm_rs* rs = nullptr;
+        EXPECT(dm_rs_create(c, 9, 2, &rs) == DM_ERR_INVALID && rs == nullptr);
+        EXPECT(dm_rs_create(c, 4, 8, &rs) == DM_OK && rs != nullptr);
+        uint8_t mat[12 * 4];
+        EXPECT(dm_rs_matrix(rs, mat) == DM_OK && mat[0] == 1 && mat[5] == 1 && mat[16] == 0x1b);
+        for (uint64_t shard : {1ull, 17ull, 4096ull, 100003ull}) {
+            std::vector<std::vector<uint8_t>> sh(12);
+            for (int j = 0; j < 4; j++) sh[j] = bytes(shard, 7000 + j + shard);
+            for (int i = 4; i < 12; i++) sh[i].assign(shard, 0);
+            std::vector<std::vector<uint8_t>> want(8, std::vector<uint8_t>(shard));
+            const uint8_t* dp[4];
+            uint8_t* wp[8];
+            void* pp[8];
+            for (int j = 0; j < 4; j++) dp[j] = sh[j].data();
+            for (int i = 0; i < 8; i++) {
+                wp[i] = want[i].data();
+                pp[i] = sh[4 + i].data();
+            }
+            EXPECT(or_rs_encode(4, 8, dp, wp, shard, 1) == 0);
+            EXPECT(dm_rs_encode(rs, reinterpret_cast<const void* const*>(dp), pp, shard) == DM_OK);
+            for (int i = 0; i < 8; i++) EXPECT(sh[4 + i] == want[i]);
+            std::vector<void*> all(12);
+            for (int i = 0; i < 12; i++) all[i] = sh[i].data();
+            int ok = 0;
+            EXPECT(dm_rs_verify(rs, all.data(), shard, &ok) == DM_OK && ok == 1);
+            auto keep = sh;
+            uint8_t present[12];
+            for (int i = 0; i < 12; i++) present[i] = (i % 3 == 1) || i == 11;   // 1,4,7,10,11
+            for (int i = 0; i < 12; i++)
+                if (!present[i]) std::fill(sh[i].begin(), sh[i].end(), 0xEE);
+            EXPECT(dm_rs_reconstruct(rs, all.data(), present, shard) == DM_OK);
+            EXPECT(sh == keep);
+            uint8_t few[12] = {1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+            EXPECT(dm_rs_reconstruct(rs, all.data(), few, shard) == DM_ERR_INVALID);
+        }
+        // Split + Encode of one odd-sized segment
+        auto seg = bytes(1001, 99);
+        std::vector<uint8_t> out(12 * 251);
+        uint64_t per = 0;
+        EXPECT(dm_rs_encode_buffer(rs, seg.data(), seg.size(), out.data(), &per) == DM_OK && per == 251);
+        EXPECT(std::memcmp(out.data(), seg.data(), seg.size()) == 0 && out[1001] == 0 && out[1003] == 0);
+        EXPECT(dm_rs_encode_buffer(rs, seg.data(), 0, out.data(), &per) == DM_ERR_EMPTY);
+        // device-resident batch: 3 segments of 4 x 4096 bytes
+        const uint64_t shard = 4096, nseg = 3;
+        auto data = bytes(nseg * 4 * shard, 4242);
+        void *dd = nullptr, *dpar = nullptr;
+        EXPECT(hipMalloc(&dd, data.size()) == hipSuccess && hipMalloc(&dpar, nseg * 8 * shard) == hipSuccess);
+        EXPECT(hipMemcpy(dd, data.data(), data.size(), hipMemcpyHostToDevice) == hipSuccess);
+        EXPECT(dm_rs_encode_device_async(rs, dd, 4 * shard, dpar, 8 * shard, shard, nseg, nullptr) == DM_OK);
+        EXPECT(dm_rs_encode_device_async(rs, (uint8_t*)dd + 1, 4 * shard, dpar, 8 * shard, shard, nseg, nullptr) ==
+               DM_ERR_INVALID);
+        EXPECT(hipDeviceSynchronize() == hipSuccess);
+        std::vector<uint8_t> par(nseg * 8 * shard);
+        EXPECT(hipMemcpy(par.data(), dpar, par.size(), hipMemcpyDeviceToHost) == hipSuccess);
+        for (uint64_t s2 = 0; s2 < nseg; s2++) {
+            const uint8_t* dp[4];
+            std::vector<std::vector<uint8_t>> want(8, std::vector<uint8_t>(shard));
+            uint8_t* wp[8];
+            for (int j = 0; j < 4; j++) dp[j] = data.data() + s2 * 4 * shard + j * shard;
+            for (int i = 0; i < 8; i++) wp[i] = want[i].data();
+            EXPECT(or_rs_encode(4, 8, dp, wp, shard, 1) == 0);
+            for (int i = 0; i < 8; i++)
+                EXPECT(std::memcmp(par.data() + s2 * 8 * shard + i * shard, want[i].data(), shard) == 0);
+        }
+        // device reconstruct of segment 0 with fragments 0, 2 and 9 lost
+        void* dev_sh[12];
+        std::vector<void*> fr(12);
+        void* dall = nullptr;
+        EXPECT(hipMalloc(&dall, 12 * shard) == hipSuccess);
+        EXPECT(hipMemcpy(dall, data.data(), 4 * shard, hipMemcpyHostToDevice) == hipSuccess);
+        EXPECT(hipMemcpy((uint8_t*)dall + 4 * shard, par.data(), 8 * shard, hipMemcpyHostToDevice) == hipSuccess);
+        EXPECT(hipMemset(dall, 0, shard) == hipSuccess);
+        for (int i = 0; i < 12; i++) dev_sh[i] = (uint8_t*)dall + i * shard;
+        uint8_t pres[12] = {0, 1, 0, 1, 1, 1, 1, 1, 1, 0, 1, 1};
+        EXPECT(dm_rs_reconstruct_device_async(rs, dev_sh, pres, shard, nullptr) == DM_OK);
+        EXPECT(hipDeviceSynchronize() == hipSuccess);
+        std::vector<uint8_t> back(12 * shard);
+        EXPECT(hipMemcpy(back.data(), dall, back.size(), hipMemcpyDeviceToHost) == hipSuccess);
+        EXPECT(std::memcmp(back.data(), data.data(), 4 * shard) == 0);
+        EXPECT(std::memcmp(back.data() + 4 * shard, par.data(), 8 * shard) == 0);
+        (void)hipFree(dall);
+        (void)hipFree(dd);
+        (void)hipFree(dpar);
+        dm_rs_destroy(rs);
     }
 
     // concurrent callers on one context
