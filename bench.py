@@ -77,7 +77,7 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
-    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs"],
+    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs", "process", "proofs"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
                          "upload: one object fed in pieces through dm_stream (hash while receiving)")
@@ -118,6 +118,10 @@ def main() -> None:
         return run_upload(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload == "rs":
         return run_rs(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "process":
+        return run_process(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "proofs":
+        return run_proofs(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload != "object":
         return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
     per_gpu = int(args.object_gib * (1 << 30))
@@ -414,6 +418,182 @@ def run_rs(args, torch, dist, world, rank, device, dev_index, gloo):
                                "sample": f"{sample} segments x {seg} B of the same data, scalar table-driven "
                                          "GF(2^8) encode (oracle/rs_oracle.c, stands in for klauspost's Go path)",
                                "parallel": {"value": round(res[max(res)], 4), "cores": max(res)}}
+    print(json.dumps(out), flush=True)
+
+
+def timed_steps(args, torch, dist, world, device, gloo, ctx, step):
+    """Warmup, then exactly args.steps steps between barrier + synchronize; max over ranks.
+    Returns (elapsed s, timed calls, sum of leaf-kernel ms, sum of whole-call ms)."""
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    n, k_sum, call_sum, _ = ctx.timing_summary()
+    ctx.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, n, k_sum, call_sum
+
+
+def run_process(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #2: cess-go-sdk FullProcessing (cipher "") of a device-resident object: zero-padded
+    32 MiB segments -> RS 4 + 8 fragments -> SHA-256 of every segment and fragment -> fid.  One
+    step = one dm_process_device_async call (RS launch + one leaf-kernel launch over 13 leaves per
+    segment + the fid tree).  Weak scaling: objects are independent, no exchange."""
+    from deoss_amd import MerkleContext
+    from deoss_amd.process import Processor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    seg = args.segment_mib << 20
+    k, m = 4, 8
+    frag = seg // k
+    length = int(args.object_gib * (1 << 30))
+    nseg = -(-length // seg)
+    ctx = MerkleContext(devices=[dev_index])
+    ctx.set_leaf_kernel(args.leaf_kernel)
+    proc = Processor(ctx, k, m, seg)
+    sptr = torch.cuda.current_stream().cuda_stream
+    obj = torch.empty(nseg * seg, dtype=torch.uint8, device=device)
+    ctx.fill_synthetic_async(obj.data_ptr(), 0, (length + 7) // 8 * 8, SEED + 0x200 * (rank + 1), sptr)
+    parity = torch.empty(nseg * m * frag, dtype=torch.uint8, device=device)
+    segh = torch.empty(nseg * 32, dtype=torch.uint8, device=device)
+    fragh = torch.empty(nseg * (k + m) * 32, dtype=torch.uint8, device=device)
+    fid = torch.empty(32, dtype=torch.uint8, device=device)
+
+    def step():
+        proc.process_device_async(obj.data_ptr(), length, parity.data_ptr(), segh.data_ptr(), fragh.data_ptr(),
+                                  fid.data_ptr(), sptr)
+
+    elapsed, n, k_sum, call_sum = timed_steps(args, torch, dist, world, device, gloo, ctx, step)
+    # parity: every segment digest and the fid (CPU, 16 threads over the same bytes), all 12
+    # fragment digests of the first and last segment (CPU restatement of Split + Encode + SHA-256)
+    orc = Oracle()
+    host = obj[:length].cpu().numpy()
+    threads = min(16, os.cpu_count() or 1)
+    padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
+    want_seg, _ = orc.root_buffer_ptr(host.ctypes.data, (nseg - 1) * seg, seg, threads, True) if nseg > 1 \
+        else (b"", None)
+    want_seg = (want_seg or b"") + orc.sha256(padded)
+    want_fid = orc.reduce(want_seg)[:32]
+    got_seg = bytes(segh.cpu().numpy())
+    got_frag = bytes(fragh.cpu().numpy())
+    frag_ok = True
+    for s_i in sorted({0, nseg - 1}):
+        sbytes = padded if s_i == nseg - 1 else host[s_i * seg:(s_i + 1) * seg].tobytes()
+        wseg, wfrag, _, _ = orc.full_processing(sbytes, seg, k, m, nthreads=threads)
+        frag_ok &= wfrag == got_frag[s_i * (k + m) * 32:(s_i + 1) * (k + m) * 32]
+    parity_ok = got_seg == want_seg and bytes(fid.cpu().numpy()) == want_fid and frag_ok
+    if rank != 0:
+        return
+    k_avg_ms = k_sum / max(n, 1)
+    hashed = nseg * seg + nseg * (k + m) * frag        # leaf-kernel bytes per launch
+    achieved = hashed / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+    kind = ctx.leaf_kernel_for(nseg * (1 + k + m))
+    out = {
+        "metric": "device-resident GiB/s of object bytes through FullProcessing (RS 4+8, SHA-256 names, fid)",
+        "value": round(length * world * args.steps / elapsed / (1 << 30), 4), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32 (SHA-256), u8 (GF(2^8))",
+        "data": "synthetic splitmix64 object generated in HBM",
+        "config": {"workload": f"{length} B object per GPU -> {nseg} segments of {seg} B -> {k}+{m} fragments "
+                               f"of {frag} B, {nseg * (1 + k + m)} SHA-256 leaves in one launch",
+                   "object_bytes": length, "segment_bytes": seg, "leaf_kernel": kind,
+                   "parallelism": f"{world} x independent"},
+        "roofline": {"bound": "hbm", "kernel": f"leaf kernel ({kind}) over segments + fragments",
+                     "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "leaf_kernel_avg_ms": round(k_avg_ms, 3), "call_avg_ms": round(call_sum / max(n, 1), 3),
+                     "algorithmic_bytes_per_launch": hashed,
+                     "regime": "latency-bound: one serial SHA-256 chain per 32 MiB segment sets the time"},
+        "parity": {"segment_digests": nseg, "fid": bytes(fid.cpu().numpy()).hex(),
+                   "fragment_digests_checked_segments": sorted({0, nseg - 1}), "bit_exact": bool(parity_ok)},
+    }
+    if world == 1 and not args.no_cpu:
+        sample = min(nseg, 2)
+        buf = host[:sample * seg].tobytes()
+        t0 = time.perf_counter()
+        orc.full_processing(buf, seg, k, m, nthreads=1)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": round(sample * seg / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
+                               "kind": "port", "sample": f"{sample} segments x {seg} B of the same object through "
+                               "oracle/process_oracle.c (SHA-NI SHA-256 + table GF(2^8) RS, serial like the SDK)"}
+    print(json.dumps(out), flush=True)
+
+
+def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #4: merkletree proofs on the GPU.  A tree of --objects leaves of --object-mib each
+    (default 2^20 x 4 KiB) is built in HBM; one step = verify every leaf's GetMerklePath proof
+    (re-hash the leaf content, fold depth node hashes, compare with the root) in one call.
+    Also reports the level build and path gather times."""
+    from deoss_amd import MerkleContext
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    n = args.objects
+    leaf = int(args.object_mib * (1 << 20))
+    ctx = MerkleContext(devices=[dev_index])
+    sptr = torch.cuda.current_stream().cuda_stream
+    obj = torch.empty(n * leaf, dtype=torch.uint8, device=device)
+    ctx.fill_synthetic_async(obj.data_ptr(), 0, n * leaf, SEED + 0x300 * (rank + 1), sptr)
+    leaves = torch.empty(n * 32, dtype=torch.uint8, device=device)
+    root = torch.empty(32, dtype=torch.uint8, device=device)
+    ctx.root_device_async(obj.data_ptr(), n * leaf, leaf, root.data_ptr(), leaves.data_ptr(), sptr)
+    nodes = torch.empty(ctx.tree_node_count(n) * 32, dtype=torch.uint8, device=device)
+    depth = ctx.tree_depth(n)
+    idx = torch.arange(n, dtype=torch.int64, device=device)
+    paths = torch.empty(n * depth * 32, dtype=torch.uint8, device=device)
+    bits = torch.empty(n * depth, dtype=torch.uint8, device=device)
+    ok = torch.zeros(n, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.tree_levels_device_async(leaves.data_ptr(), n, nodes.data_ptr(), sptr)
+    torch.cuda.synchronize()
+    t_levels = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ctx.merkle_paths_device_async(leaves.data_ptr(), nodes.data_ptr(), n, idx.data_ptr(), n, paths.data_ptr(),
+                                  bits.data_ptr(), sptr)
+    torch.cuda.synchronize()
+    t_paths = time.perf_counter() - t0
+    base = obj.data_ptr()
+    ptrs = [base + i * leaf for i in range(n)]
+    lens = [leaf] * n
+
+    def step():
+        ctx.verify_paths_device_async(ptrs, lens, n, paths.data_ptr(), bits.data_ptr(), depth, root.data_ptr(), 0,
+                                      ok.data_ptr(), sptr)
+
+    elapsed, calls, _, _ = timed_steps(args, torch, dist, world, device, gloo, ctx, step)
+    all_ok = int(ok.sum().item()) == n
+    orc = Oracle()
+    host = obj.cpu().numpy()
+    _, want_root = orc.root_buffer_ptr(host.ctypes.data, n * leaf, leaf, min(16, os.cpu_count() or 1))
+    root_ok = bytes(root.cpu().numpy()) == want_root and bytes(nodes[-32:].cpu().numpy()) == want_root
+    if rank != 0:
+        return
+    out = {
+        "metric": "GetMerklePath proofs verified per second (leaf re-hash + path fold on the GPU)",
+        "value": round(n * world * args.steps / elapsed, 1), "unit": "proofs/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic splitmix64 leaves generated in HBM",
+        "config": {"workload": f"{n} leaves x {leaf} B, depth {depth}, every leaf's proof per step",
+                   "leaves": n, "leaf_bytes": leaf, "depth": depth},
+        "levels_ms": round(t_levels * 1e3, 3), "paths_ms": round(t_paths * 1e3, 3),
+        "content_GiBps": round(n * leaf * world * args.steps / elapsed / (1 << 30), 3),
+        "parity": {"all_proofs_verify": all_ok, "root_matches_cpu": root_ok, "bit_exact": all_ok and root_ok},
+    }
     print(json.dumps(out), flush=True)
 
 

@@ -35,6 +35,9 @@ EXPORTS = (
     "dm_timing_summary",
     "dm_rs_create", "dm_rs_destroy", "dm_rs_matrix", "dm_rs_encode", "dm_rs_encode_buffer", "dm_rs_reconstruct",
     "dm_rs_verify", "dm_rs_encode_device_async", "dm_rs_reconstruct_device_async",
+    "dm_process_device_async", "dm_process_buffer",
+    "dm_tree_node_count", "dm_tree_depth", "dm_tree_levels_device_async", "dm_tree_levels",
+    "dm_merkle_paths_device_async", "dm_merkle_paths", "dm_verify_paths_device_async", "dm_verify_paths",
 )
 
 
@@ -86,6 +89,16 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_rs_verify": ([vp, pvp, u64, ctypes.POINTER(i32)], i32),
         "dm_rs_encode_device_async": ([vp, vp, u64, vp, u64, u64, u64, vp], i32),
         "dm_rs_reconstruct_device_async": ([vp, pvp, vp, u64, vp], i32),
+        "dm_process_device_async": ([vp, vp, u64, u64, vp, vp, vp, vp, vp], i32),
+        "dm_process_buffer": ([vp, vp, u64, u64, vp, vp, vp, vp], i32),
+        "dm_tree_node_count": ([u64], u64),
+        "dm_tree_depth": ([u64], u32),
+        "dm_tree_levels_device_async": ([vp, vp, u64, vp, vp], i32),
+        "dm_tree_levels": ([vp, vp, u64, vp], i32),
+        "dm_merkle_paths_device_async": ([vp, vp, vp, u64, vp, u64, vp, vp, vp], i32),
+        "dm_merkle_paths": ([vp, vp, u64, vp, u64, vp, vp], i32),
+        "dm_verify_paths_device_async": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
+        "dm_verify_paths": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

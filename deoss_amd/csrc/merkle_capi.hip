@@ -95,6 +95,7 @@ struct Dev {
     hipStream_t stream = nullptr;       // compute stream
     hipStream_t copy = nullptr;         // H2D stream
     DevBuf data, nodes_a, nodes_b, leaves, tab_addr, tab_len, tab_first, tab_ids, root, gather;
+    DevBuf proof_paths, proof_bits, proof_roots;   // host-API proof staging (tree_capi.inl)
     PinnedBuf stage[2];
     PinnedBuf htab;                     // pinned bounce buffer for per-call index tables
     uint64_t htab_used = 0;
@@ -601,7 +602,7 @@ void destroy_device(Dev& d) {
     if (hipSetDevice(d.id) != hipSuccess) return;
     (void)hipDeviceSynchronize();
     for (DevBuf* b : {&d.data, &d.nodes_a, &d.nodes_b, &d.leaves, &d.tab_addr, &d.tab_len, &d.tab_first, &d.tab_ids,
-                      &d.root, &d.gather})
+                      &d.root, &d.gather, &d.proof_paths, &d.proof_bits, &d.proof_roots})
         b->release();
     d.stage[0].release();
     d.stage[1].release();
@@ -1018,3 +1019,5 @@ int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t*
 // Streaming (incremental) roots: dm_stream_* (shares the helpers above).
 #include "merkle_stream.inl"
 #include "rs_capi.inl"
+#include "process_capi.inl"
+#include "tree_capi.inl"

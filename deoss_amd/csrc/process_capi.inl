@@ -1,0 +1,136 @@
+// process_capi.inl -- FullProcessing on the GPU (dm_process_*, include/deoss_merkle.h).
+// Part of merkle_capi.hip (included after rs_capi.inl; shares dm_ctx, Dev, dm_rs and the helpers).
+//
+// Replaces cess-go-sdk process.FullProcessing(file, cipher = "", savedir) (go.mod:8), which every
+// upload handler runs to get the fid and the fragment names (node/objectHandler.go:168,
+// node/fileHandler.go:771, node/filesHandler.go:201, node/resumeHandler.go:326,
+// node/tracker.go:767-769) and the fragment download path re-runs (node/fileHandler.go:964,997).
+// One call, all on the device:
+//   1. zero the last segment's padding in place (hipMemsetAsync);
+//   2. rs_code_kernel codes every segment into its parity fragments (one launch, all segments);
+//   3. ONE table-mode leaf-kernel launch hashes the nseg segments (32 MiB leaves, listed first so
+//      they start first) and the nseg x (data + parity) fragments (8 MiB leaves) together: the
+//      segment chains set the time, the fragment chains run beside them on otherwise idle SIMDs;
+//   4. the segment digests reduce to the fid (K2 / finish).
+// Oracle: oracle/process_oracle.c (restated composition; parity of the composition unpinned).
+
+namespace {
+
+int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uint64_t segment, uint8_t* parity,
+                uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t* fid) {
+    dm_ctx* c = r->c;
+    const int k = r->k, m = r->m, total = k + m;
+    const uint64_t nseg = ceil_div(len, segment), frag = segment / (uint64_t)k;
+    RC_TRY(begin_call(c, d, s));
+    if (nseg * segment > len) HIP_TRY(hipMemsetAsync(obj + len, 0, nseg * segment - len, s));
+    dm::RsArgs a{};
+    for (int j = 0; j < k; j++) a.in[j] = obj + (uint64_t)j * frag;
+    for (int i = 0; i < m; i++) a.out[i] = parity + (uint64_t)i * frag;
+    a.in_seg_stride = segment;
+    a.out_seg_stride = (uint64_t)m * frag;
+    a.units_per_seg = frag / 16;
+    a.nseg = nseg;
+    a.table = static_cast<const uint2*>(r->enc_tab.p);
+    a.nout = (uint32_t)m;
+    launch_rs(d, s, k, a);
+    HIP_TRY(hipGetLastError());
+    // leaf table: segments first, then fragments in (segment, shard) order
+    const uint64_t T = nseg * (1 + (uint64_t)total);
+    std::vector<uint64_t> addr(T), lens(T);
+    for (uint64_t i = 0; i < nseg; i++) {
+        addr[i] = reinterpret_cast<uint64_t>(obj + i * segment);
+        lens[i] = segment;
+    }
+    for (uint64_t i = 0; i < nseg; i++)
+        for (int j = 0; j < total; j++) {
+            const uint64_t t = nseg + i * total + j;
+            addr[t] = reinterpret_cast<uint64_t>(j < k ? obj + i * segment + (uint64_t)j * frag
+                                                       : parity + (i * m + (j - k)) * frag);
+            lens[t] = frag;
+        }
+    RC_TRY(tables_begin(c, d, T * 16 + 1024));
+    HIP_TRY(d.leaves.ensure(T * 32));
+    RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), T * 8));
+    RC_TRY(upload(c, d, s, d.tab_len, lens.data(), T * 8));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(d.tab_addr.p);
+    la.lens = static_cast<const uint64_t*>(d.tab_len.p);
+    la.nleaves = T;
+    la.byte_end = ~0ull;
+    la.digests = d.leaves.u8();
+    hipEvent_t* tr = timing_record(c, d);
+    if (tr) HIP_TRY(hipEventRecord(tr[0], s));
+    RC_TRY(launch_leaves(c, s, la, true, true, pick_leaf_kernel(c, d, T)));
+    if (tr) HIP_TRY(hipEventRecord(tr[1], s));
+    RC_TRY(finish(c, d, s, d.leaves.u8(), nseg, true, fid));
+    if (tr) HIP_TRY(hipEventRecord(tr[2], s));
+    if (seg_hashes) HIP_TRY(hipMemcpyAsync(seg_hashes, d.leaves.p, nseg * 32, hipMemcpyDeviceToDevice, s));
+    if (frag_hashes)
+        HIP_TRY(hipMemcpyAsync(frag_hashes, d.leaves.u8() + nseg * 32, nseg * total * 32, hipMemcpyDeviceToDevice, s));
+    return DM_OK;
+}
+
+int process_check(dm_rs* r, uint64_t len, uint64_t segment) {
+    dm_ctx* c = r->c;
+    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    if (segment == 0 || segment % (16ull * (uint64_t)r->k))
+        return fail(c, DM_ERR_INVALID, "segment size %llu must be a non-zero multiple of 16 x %d data shards",
+                    (unsigned long long)segment, r->k);
+    return DM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dm_process_device_async(dm_rs* r, void* dev_obj, uint64_t len, uint64_t segment, void* dev_parity,
+                            void* dev_seg_hashes, void* dev_frag_hashes, void* dev_fid, void* stream) {
+    if (!r) return DM_ERR_INVALID;
+    dm_ctx* c = r->c;
+    std::lock_guard<std::mutex> lk(c->mu);
+    RC_TRY(process_check(r, len, segment));
+    if (!dev_obj || !dev_parity || !dev_fid || !is_aligned16(dev_obj) || !is_aligned16(dev_parity))
+        return fail(c, DM_ERR_INVALID, "dm_process_device_async: need 16-byte aligned object and parity buffers");
+    Dev& d = c->devs[0];
+    return process_dev(r, d, pick_stream(d, stream), static_cast<uint8_t*>(dev_obj), len, segment,
+                       static_cast<uint8_t*>(dev_parity), static_cast<uint8_t*>(dev_seg_hashes),
+                       static_cast<uint8_t*>(dev_frag_hashes), static_cast<uint8_t*>(dev_fid));
+}
+
+int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment, void* frags_out,
+                      uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t fid[32]) {
+    if (!r) return DM_ERR_INVALID;
+    dm_ctx* c = r->c;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (!fid || (!host && len)) return fail(c, DM_ERR_INVALID, "dm_process_buffer: null argument");
+    RC_TRY(process_check(r, len, segment));
+    Dev& d = c->devs[0];
+    hipStream_t s = d.stream;
+    RC_TRY(begin_call(c, d, s));
+    const int k = r->k, m = r->m, total = k + m;
+    const uint64_t nseg = ceil_div(len, segment), frag = segment / (uint64_t)k;
+    HIP_TRY(d.data.ensure(nseg * segment));
+    std::vector<uint64_t> addr;
+    const void* src = host;
+    RC_TRY(pack_chunks(c, d, &src, &len, 1, addr));   // H2D into d.data (offset 0)
+    HIP_TRY(r->work.ensure(nseg * (uint64_t)m * frag + (nseg * (1 + (uint64_t)total) + 1) * 32));
+    uint8_t* parity = r->work.u8();
+    uint8_t* dig = parity + nseg * (uint64_t)m * frag;   // seg hashes, frag hashes, fid
+    RC_TRY(process_dev(r, d, s, d.data.u8(), len, segment, parity, dig, dig + nseg * 32,
+                       dig + nseg * (1 + (uint64_t)total) * 32));
+    HIP_TRY(hipMemcpyAsync(fid, dig + nseg * (1 + (uint64_t)total) * 32, 32, hipMemcpyDeviceToHost, s));
+    if (seg_hashes) HIP_TRY(hipMemcpyAsync(seg_hashes, dig, nseg * 32, hipMemcpyDeviceToHost, s));
+    if (frag_hashes) HIP_TRY(hipMemcpyAsync(frag_hashes, dig + nseg * 32, nseg * total * 32, hipMemcpyDeviceToHost, s));
+    if (frags_out) {
+        uint8_t* o = static_cast<uint8_t*>(frags_out);
+        for (uint64_t i = 0; i < nseg; i++) {
+            HIP_TRY(hipMemcpyAsync(o + i * total * frag, d.data.u8() + i * segment, segment, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(o + i * total * frag + segment, parity + i * m * frag, m * frag,
+                                   hipMemcpyDeviceToHost, s));
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return DM_OK;
+}
+
+}  // extern "C"

@@ -8,11 +8,14 @@ Mirrors the reference Go API (same names, argument meaning and error behaviour):
 * ``HashTreeContent`` -- ``common/hashtree/hashtree.go:18-35`` (``CalculateHash``, ``Equals``).
 * ``MerkleTree`` / ``Node`` -- the parts of ``cbergoon/merkletree`` v0.2.0 the reference test reads:
   ``Leafs`` (n entries, n+1 when n is odd: the last leaf duplicated with ``dup=True``),
-  ``MerkleRoot()`` and ``Root``.
+  ``MerkleRoot()`` and ``Root``; plus the proof API ``GetMerklePath(content)``,
+  ``VerifyContent(content)`` and ``VerifyTree()``, whose levels, paths and
+  proof folds run on the GPU (``dm_tree_levels``, ``dm_merkle_paths``, ``dm_verify_paths``).
 
-Deviation (documented in DESIGN.md): interior nodes are not materialised (the GPU reduces the
-tree in LDS); ``Root.Left``/``Right`` are ``None``.  ``Leafs[i].C.Equals`` compares chunk bytes
-when the content was kept (``keep_content=True``) and digests otherwise.
+Deviation (documented in DESIGN.md): interior nodes are not ``Node`` objects (the root comes from
+the fused leaf kernel; the levels are built on the GPU the first time a proof asks for them);
+``Root.Left``/``Right`` are ``None``.  ``Leafs[i].C.Equals`` compares chunk bytes when the
+content was kept (``keep_content=True``) and digests otherwise.
 
 Additive entry points: ``NewHashTreeFromBuffer(buf, chunkSize)`` (the upload-handler host
 buffer path) and ``NewHashTreesBatch(objects, chunkSize)``.
@@ -76,19 +79,85 @@ class Node:
 class MerkleTree:
     Root: Node
     Leafs: List[Node] = field(default_factory=list)
+    ctx: Optional[MerkleContext] = None
 
     def MerkleRoot(self) -> bytes:
         return self.Root.Hash
 
+    def _ctx(self) -> MerkleContext:
+        return self.ctx or default_context()
 
-def _build(leaf_digests: bytes, root: bytes, contents: Sequence[Optional[bytes]]) -> MerkleTree:
+    def _digests(self) -> bytes:
+        return b"".join(l.Hash for l in self.Leafs if not l.dup)
+
+    def _find(self, content: HashTreeContent) -> Tuple[int, Optional[Exception]]:
+        """Index of the first leaf whose content Equals `content` (-1: none), as merkletree scans."""
+        for i, l in enumerate(self.Leafs):
+            ok, err = l.C.Equals(content)
+            if err is not None:
+                return -1, err
+            if ok:
+                return i, None
+        return -1, None
+
+    def GetMerklePath(self, content: HashTreeContent
+                      ) -> Tuple[Optional[List[bytes]], Optional[List[int]], Optional[Exception]]:
+        """merkletree GetMerklePath: sibling digests leaf -> root and their indices (1 = the
+        sibling is the right child); (None, None, None) when no leaf holds `content`."""
+        i, err = self._find(content)
+        if err is not None or i < 0:
+            return None, None, err
+        try:
+            (path, bits), = self._ctx().merkle_paths(self._digests(), [i])
+        except DeossMerkleError as e:
+            return None, None, e
+        return path, bits, None
+
+    def VerifyContent(self, content: HashTreeContent) -> Tuple[bool, Optional[Exception]]:
+        """merkletree VerifyContent: `content` is a leaf and its branch hashes up to the root."""
+        i, err = self._find(content)
+        if err is not None or i < 0:
+            return False, err
+        try:
+            c = self._ctx()
+            (path, bits), = c.merkle_paths(self._digests(), [i])
+            data = content.x if content.x is not None else None
+            if data is None:   # digest-only content: fold the stored digest instead of re-hashing
+                return self._fold(content.CalculateHash()[0], path, bits) == self.Root.Hash, None
+            return c.verify_paths([data], [path], [bits], [self.Root.Hash])[0], None
+        except DeossMerkleError as e:
+            return False, e
+
+    def _fold(self, h: bytes, path: List[bytes], bits: List[int]) -> bytes:
+        # digest-only proof fold: the tree over [h, sibling] pairs, one GPU level per step
+        c = self._ctx()
+        for sib, b in zip(path, bits):
+            h = c.tree_root(h + sib if b == 1 else sib + h)
+        return h
+
+    def VerifyTree(self) -> Tuple[bool, Optional[Exception]]:
+        """merkletree VerifyTree: every leaf re-hashed from its content, the root recomputed."""
+        try:
+            c = self._ctx()
+            real = [l for l in self.Leafs if not l.dup]
+            if all(l.C is not None and l.C.x is not None for l in real):
+                _, root = c.root_chunks([l.C.x for l in real])
+            else:
+                root = c.tree_root(b"".join(l.C.CalculateHash()[0] for l in real))
+            return root == self.Root.Hash, None
+        except DeossMerkleError as e:
+            return False, e
+
+
+def _build(leaf_digests: bytes, root: bytes, contents: Sequence[Optional[bytes]],
+           ctx: Optional[MerkleContext] = None) -> MerkleTree:
     n = len(leaf_digests) // 32
     leafs = [Node(Hash=leaf_digests[32 * i:32 * i + 32], C=HashTreeContent(contents[i], leaf_digests[32 * i:32 * i + 32]),
                   leaf=True) for i in range(n)]
     if n % 2 == 1:   # merkletree v0.2.0 buildWithContent: duplicate the last leaf
         last = leafs[-1]
         leafs.append(Node(Hash=last.Hash, C=last.C, leaf=True, dup=True))
-    return MerkleTree(Root=Node(Hash=root), Leafs=leafs)
+    return MerkleTree(Root=Node(Hash=root), Leafs=leafs, ctx=ctx)
 
 
 def NewHashTree(chunkPath: Sequence[str], ctx: Optional[MerkleContext] = None,
@@ -106,7 +175,7 @@ def NewHashTree(chunkPath: Sequence[str], ctx: Optional[MerkleContext] = None,
         for i, p in enumerate(chunkPath):
             with open(p, "rb") as f:
                 contents[i] = f.read()
-    return _build(b"".join(leaves), root, contents), None
+    return _build(b"".join(leaves), root, contents, c), None
 
 
 def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContext] = None
@@ -120,7 +189,7 @@ def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContex
     except DeossMerkleError as e:
         return None, e
     n = len(leaves) // 32
-    return _build(leaves, root, [None] * n), None
+    return _build(leaves, root, [None] * n, c), None
 
 
 def NewHashTreesBatch(objects: Sequence[bytes], chunkSize: int, ctx: Optional[MerkleContext] = None

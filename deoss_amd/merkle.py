@@ -10,6 +10,7 @@ torch's own kernels and copies on that stream.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 from ._lib import DM_ERR_EMPTY, DeossMerkleError, load_library
@@ -27,10 +28,14 @@ class MerkleContext:
         if rc != 0:
             raise DeossMerkleError(rc, f"dm_create: {self._L.dm_strerror(rc).decode()}")
         self._h = h
+        # objects holding C handles that point into this context (dm_rs coders): closed first
+        self._children = weakref.WeakSet()
 
     # -- lifecycle -------------------------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
+            for child in list(getattr(self, "_children", ())):
+                child.close()
             self._L.dm_destroy(self._h)
             self._h = None
 
@@ -154,6 +159,92 @@ class MerkleContext:
     def fill_synthetic_async(self, dev_ptr: int, off: int, nbytes: int, seed: int, stream: int = 0) -> None:
         self._check(self._L.dm_fill_synthetic_async(self._h, ctypes.c_void_p(dev_ptr), off, nbytes, seed,
                                                     ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
+
+    # -- tree levels and proofs (merkletree GetMerklePath / VerifyContent / VerifyTree) ----------
+    def tree_node_count(self, n: int) -> int:
+        return self._L.dm_tree_node_count(n)
+
+    def tree_depth(self, n: int) -> int:
+        return self._L.dm_tree_depth(n)
+
+    def tree_levels(self, leaf_digests: bytes) -> bytes:
+        """Levels 1 .. root over the leaf digests, level-major (the root is the last 32 bytes)."""
+        n = len(leaf_digests) // 32
+        if n == 0:
+            raise DeossMerkleError(DM_ERR_EMPTY, "Empty data")
+        out = ctypes.create_string_buffer(32 * self.tree_node_count(n))
+        self._check(self._L.dm_tree_levels(self._h, bytes(leaf_digests), n, out), "dm_tree_levels")
+        return out.raw
+
+    def tree_root(self, leaf_digests: bytes) -> bytes:
+        """Root of the tree over leaf digests (the fid of a list of segment digests)."""
+        return self.tree_levels(leaf_digests)[-32:]
+
+    def tree_levels_device_async(self, dev_leaves: int, n: int, dev_nodes: int, stream: int = 0) -> None:
+        self._check(self._L.dm_tree_levels_device_async(self._h, ctypes.c_void_p(dev_leaves), n,
+                                                        ctypes.c_void_p(dev_nodes), ctypes.c_void_p(stream or None)),
+                    "dm_tree_levels_device_async")
+
+    def merkle_paths(self, leaf_digests: bytes, indices: Sequence[int]) -> List[Tuple[List[bytes], List[int]]]:
+        """GetMerklePath for each leaf index: (sibling digests, bits) with bits[i] = 1 when the
+        sibling is the right child (merkletree's index convention)."""
+        n = len(leaf_digests) // 32
+        q = len(indices)
+        depth = self.tree_depth(n)
+        idx = (ctypes.c_uint64 * max(q, 1))(*indices)
+        paths = ctypes.create_string_buffer(max(32 * depth * q, 32))
+        bits = ctypes.create_string_buffer(max(depth * q, 1))
+        self._check(self._L.dm_merkle_paths(self._h, bytes(leaf_digests), n, idx, q, paths, bits), "dm_merkle_paths")
+        out = []
+        for t in range(q):
+            p = paths.raw[32 * depth * t:32 * depth * (t + 1)]
+            out.append(([p[32 * l:32 * l + 32] for l in range(depth)], list(bits.raw[depth * t:depth * (t + 1)])))
+        return out
+
+    def merkle_paths_device_async(self, dev_leaves: int, dev_nodes: int, n: int, dev_idx: int, q: int,
+                                  dev_paths: int, dev_bits: int, stream: int = 0) -> None:
+        self._check(self._L.dm_merkle_paths_device_async(self._h, ctypes.c_void_p(dev_leaves),
+                                                         ctypes.c_void_p(dev_nodes), n, ctypes.c_void_p(dev_idx), q,
+                                                         ctypes.c_void_p(dev_paths), ctypes.c_void_p(dev_bits),
+                                                         ctypes.c_void_p(stream or None)),
+                    "dm_merkle_paths_device_async")
+
+    def verify_paths(self, contents: Sequence[bytes], paths: Sequence[Sequence[bytes]], bits: Sequence[Sequence[int]],
+                     roots: Sequence[bytes]) -> List[bool]:
+        """ok[t]: SHA-256(contents[t]) folded with its path equals roots[t] (one root: shared)."""
+        q = len(contents)
+        if q == 0:
+            return []
+        depth = len(paths[0])
+        if any(len(p) != depth for p in paths) or any(len(b) != depth for b in bits):
+            raise DeossMerkleError(-2, "every path needs the same depth")
+        ptrs = (ctypes.c_void_p * q)()
+        lens = (ctypes.c_uint64 * q)()
+        keep = []
+        for i, c in enumerate(contents):
+            b = ctypes.create_string_buffer(bytes(c), max(len(c), 1))
+            keep.append(b)
+            ptrs[i] = ctypes.cast(b, ctypes.c_void_p)
+            lens[i] = len(c)
+        pb = b"".join(b"".join(p) for p in paths)
+        bb = bytes(x for bl in bits for x in bl)
+        shared = len(roots) == 1
+        rb = b"".join(roots)
+        ok = ctypes.create_string_buffer(q)
+        self._check(self._L.dm_verify_paths(self._h, ptrs, lens, q, pb, bb, depth, rb, 0 if shared else 32, ok),
+                    "dm_verify_paths")
+        return [bool(x) for x in ok.raw]
+
+    def verify_paths_device_async(self, dev_contents: Sequence[int], lens: Sequence[int], q: int, dev_paths: int,
+                                  dev_bits: int, depth: int, dev_roots: int, root_stride: int, dev_ok: int,
+                                  stream: int = 0) -> None:
+        ptrs = (ctypes.c_void_p * max(q, 1))(*dev_contents)
+        ls = (ctypes.c_uint64 * max(q, 1))(*lens)
+        self._check(self._L.dm_verify_paths_device_async(self._h, ptrs, ls, q, ctypes.c_void_p(dev_paths),
+                                                         ctypes.c_void_p(dev_bits), depth, ctypes.c_void_p(dev_roots),
+                                                         root_stride, ctypes.c_void_p(dev_ok),
+                                                         ctypes.c_void_p(stream or None)),
+                    "dm_verify_paths_device_async")
 
     # -- streaming -------------------------------------------------------------------------------
     def open_stream(self, chunk: int) -> "MerkleStream":

@@ -1,0 +1,140 @@
+"""Python mirror of cess-go-sdk ``process.FullProcessing`` backed by the GPU pipeline (``dm_process_*``).
+
+DeOSS computes every file id ("fid") and fragment name with
+``process.FullProcessing(file, cipher, savedir) ([]chain.SegmentDataInfo, fid string, error)``
+from cess-go-sdk (``go.mod:8``; not vendored): ``node/objectHandler.go:168``,
+``node/fileHandler.go:771``, ``node/filesHandler.go:201``, ``node/resumeHandler.go:326``,
+``node/tracker.go:767-769`` and the fragment download path ``node/fileHandler.go:964,997``.
+:func:`FullProcessing` keeps that signature and result shape:
+
+* the file is cut into ``SEGMENT_SIZE`` (chain.SegmentSize, 32 MiB) segments, the last one
+  zero-padded;
+* each segment becomes ``DATA_SHARDS + PAR_SHARDS`` fragments of ``FRAGMENT_SIZE`` (8 MiB) with
+  the klauspost Reed-Solomon coder, written to ``savedir/<hex SHA-256 of the fragment>``;
+* ``SegmentDataInfo.SegmentHash`` is ``savedir/<hex SHA-256 of the segment>`` and
+  ``SegmentDataInfo.FragmentHash`` the fragment paths, data fragments first (the handlers open
+  them by path and match ``filepath.Base`` against a requested hash, ``node/fileHandler.go:967-969``);
+* the fid is the hex ``common/hashtree`` root over the segments.
+
+Coding, hashing and the tree run on the GPU; there is no CPU fallback.  Deviations:
+the segment files themselves are not written (their bytes are the data fragments in order), and
+a non-empty ``cipher`` is rejected (the AES branch is not implemented).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+from ._lib import DM_ERR_EMPTY, DM_ERR_INVALID, DeossMerkleError
+from .merkle import MerkleContext
+from .reedsolomon import DATA_SHARDS, PAR_SHARDS, Encoder
+
+SEGMENT_SIZE = 32 << 20                       # chain.SegmentSize
+FRAGMENT_SIZE = SEGMENT_SIZE // DATA_SHARDS   # chain.FragmentSize (8 MiB; node/tracker.go:250 "96M")
+WINDOW_SEGMENTS = 64                          # segments per GPU call (2 GiB of file, 6 GiB of fragments)
+
+
+@dataclass
+class SegmentDataInfo:
+    """chain.SegmentDataInfo: the segment's path name and its fragments' path names."""
+    SegmentHash: str = ""
+    FragmentHash: List[str] = field(default_factory=list)
+
+
+class Processor:
+    """One GPU pipeline (``dm_rs`` coder + context) for FullProcessing calls."""
+
+    def __init__(self, ctx: Optional[MerkleContext] = None, data_shards: int = DATA_SHARDS,
+                 parity_shards: int = PAR_SHARDS, segment: int = SEGMENT_SIZE):
+        self.ctx = ctx or MerkleContext()
+        self.enc = Encoder(self.ctx, data_shards, parity_shards)
+        self.segment = segment
+        self.k, self.m = data_shards, parity_shards
+        self.frag = segment // data_shards
+
+    def close(self) -> None:
+        self.enc.close()
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc == DM_ERR_EMPTY:
+            raise DeossMerkleError(rc, "Empty data")
+        self.enc._check(rc, what)
+
+    # -- raw pipeline ----------------------------------------------------------------------------
+    def process_buffer(self, buf, want_frags: bool = True) -> Tuple[bytes, bytes, bytes, Optional[bytes]]:
+        """One ``dm_process_buffer`` call: (segment digests, fragment digests, fid, fragments)."""
+        n = len(buf)
+        nseg = (n + self.segment - 1) // self.segment if n else 0
+        total = self.k + self.m
+        seg = ctypes.create_string_buffer(max(32 * nseg, 32))
+        frag = ctypes.create_string_buffer(max(32 * nseg * total, 32))
+        fid = ctypes.create_string_buffer(32)
+        frags = ctypes.create_string_buffer(nseg * total * self.frag) if (want_frags and nseg) else None
+        src = buf if isinstance(buf, ctypes.Array) else ctypes.create_string_buffer(bytes(buf), max(n, 1))
+        L = self.ctx._L
+        self._check(L.dm_process_buffer(self.enc._h, src, n, self.segment, frags, seg, frag, fid),
+                    "dm_process_buffer")
+        return seg.raw[:32 * nseg], frag.raw[:32 * nseg * total], fid.raw, (frags.raw if frags is not None else None)
+
+    def process_device_async(self, obj_ptr: int, length: int, parity_ptr: int, seg_hash_ptr: int,
+                             frag_hash_ptr: int, fid_ptr: int, stream: int = 0) -> None:
+        """``dm_process_device_async``: object already in HBM (room for whole segments)."""
+        self._check(self.ctx._L.dm_process_device_async(self.enc._h, obj_ptr, length, self.segment, parity_ptr,
+                                                        seg_hash_ptr or None, frag_hash_ptr or None, fid_ptr,
+                                                        stream), "dm_process_device_async")
+
+    # -- FullProcessing ----------------------------------------------------------------------------
+    def FullProcessing(self, file: str, cipher: str, savedir: str
+                       ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
+        if cipher:
+            return None, "", DeossMerkleError(DM_ERR_INVALID, "cipher is not supported by the GPU pipeline")
+        try:
+            size = os.path.getsize(file)
+        except OSError as e:
+            return None, "", e
+        if size == 0:
+            return None, "", DeossMerkleError(-1, "Empty data")
+        os.makedirs(savedir, exist_ok=True)
+        info: List[SegmentDataInfo] = []
+        seg_digests = []
+        window = WINDOW_SEGMENTS * self.segment
+        total = self.k + self.m
+        try:
+            with open(file, "rb") as f:
+                while True:
+                    buf = f.read(window)
+                    if not buf:
+                        break
+                    segd, fragd, fid, frags = self.process_buffer(buf, want_frags=True)
+                    for s in range(len(segd) // 32):
+                        seg_digests.append(segd[32 * s:32 * s + 32])
+                        names = []
+                        for j in range(total):
+                            t = s * total + j
+                            path = os.path.join(savedir, fragd[32 * t:32 * t + 32].hex())
+                            if not os.path.exists(path):
+                                with open(path, "wb") as out:
+                                    out.write(frags[t * self.frag:(t + 1) * self.frag])
+                            names.append(path)
+                        info.append(SegmentDataInfo(os.path.join(savedir, segd[32 * s:32 * s + 32].hex()), names))
+                    if len(buf) < window:
+                        break
+        except (OSError, DeossMerkleError) as e:
+            return None, "", e
+        if len(seg_digests) * self.segment > window:   # several windows: tree over all segments
+            fid = self.ctx.tree_root(b"".join(seg_digests))
+        return info, fid.hex(), None
+
+
+_default: Optional[Processor] = None
+
+
+def FullProcessing(file: str, cipher: str, savedir: str
+                   ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
+    """process.FullProcessing(file, cipher, savedir) on the default GPU pipeline."""
+    global _default
+    if _default is None:
+        _default = Processor()
+    return _default.FullProcessing(file, cipher, savedir)

@@ -33,6 +33,7 @@ class Encoder:
         rc = self._L.dm_rs_create(ctx._h, data_shards, parity_shards, ctypes.byref(h))
         ctx._check(rc, "dm_rs_create")
         self._h = h
+        ctx._children.add(self)   # the context destroys this coder before itself
         self.data_shards = data_shards
         self.parity_shards = parity_shards
         self.total_shards = data_shards + parity_shards

@@ -154,6 +154,63 @@ int dm_rs_encode_device_async(dm_rs *rs, const void *data, uint64_t data_stride,
 int dm_rs_reconstruct_device_async(dm_rs *rs, void *const *shards, const uint8_t *present, uint64_t shard,
                                    void *stream);
 
+/* ---- FullProcessing: segments -> fragments -> names -> fid -----------------
+ * Replaces cess-go-sdk process.FullProcessing(file, cipher = "", savedir) (go.mod:8; called at
+ * node/fileHandler.go:771, node/objectHandler.go:168, node/filesHandler.go:201,
+ * node/resumeHandler.go:326, node/tracker.go:767-769, node/fileHandler.go:964,997).  The object is
+ * cut into `segment`-byte segments (chain.SegmentSize = 32 MiB; the last one zero-padded); each
+ * segment is coded by `rs` (klauspost Split + Encode: rs data shards = the segment in order, then
+ * the parity shards, `segment / data` bytes each = chain.FragmentSize); every segment and fragment
+ * is named by its SHA-256 (its file name in savedir is the hex digest); the fid is the
+ * common/hashtree root over the segments (NewHashTree(segmentPaths), types.go:19-39).  Coding,
+ * hashing and the tree all run on the GPU.  Empty object -> DM_ERR_EMPTY.  The cipher branch
+ * (AES before coding) is not implemented. */
+
+/* Device-resident form on rs's context.  dev_obj holds len bytes with room for nseg * segment
+ * (nseg = ceil(len / segment)); the padding [len, nseg * segment) is zeroed in place.  segment must
+ * be a multiple of 16 * data shards; dev_obj, dev_parity 16-byte aligned.  Writes
+ *   dev_parity       nseg x parity x frag bytes (segment s, parity fragment i at (s*parity + i)*frag)
+ *   dev_seg_hashes   nseg x 32 (nullable)
+ *   dev_frag_hashes  nseg x (data + parity) x 32, data fragments first (nullable)
+ *   dev_fid          32 bytes
+ * in stream order on `stream`. */
+int dm_process_device_async(dm_rs *rs, void *dev_obj, uint64_t len, uint64_t segment, void *dev_parity,
+                            void *dev_seg_hashes, void *dev_frag_hashes, void *dev_fid, void *stream);
+/* Host form (synchronous).  frags_out (nullable) receives nseg x (data + parity) x frag bytes,
+ * segment-major, data fragments first (the zero-padded segment bytes).  seg_hashes nseg x 32 and
+ * frag_hashes nseg x (data + parity) x 32 are nullable; fid is required. */
+int dm_process_buffer(dm_rs *rs, const void *host, uint64_t len, uint64_t segment, void *frags_out,
+                      uint8_t *seg_hashes, uint8_t *frag_hashes, uint8_t fid[32]);
+
+/* ---- Merkle tree levels and proofs ----------------------------------------
+ * cbergoon/merkletree v0.2.0 (go.mod:10) keeps every node of the tree NewHashTree returns
+ * (common/hashtree/types.go:38) for GetMerklePath, VerifyContent and VerifyTree.  Here the nodes
+ * live level-major: level 1 (ceil(n/2) nodes), level 2, ..., the root last, 32 bytes each
+ * (dm_tree_node_count(n) nodes); the n leaf digests are level 0.  Every leaf's path has
+ * dm_tree_depth(n) = max(1, ceil(log2 n)) steps.  Path bits follow GetMerklePath: 1 = the sibling
+ * is the right child (taken whenever the left child's digest equals the current node's, as the
+ * reference compares hashes), 0 = the sibling is the left child. */
+uint64_t dm_tree_node_count(uint64_t n);
+uint32_t dm_tree_depth(uint64_t n);
+/* All levels over n leaf digests (device, stream-ordered / host, synchronous). */
+int dm_tree_levels_device_async(dm_ctx *ctx, const void *dev_leaves, uint64_t n, void *dev_nodes, void *stream);
+int dm_tree_levels(dm_ctx *ctx, const uint8_t *leaf_digests, uint64_t n, uint8_t *nodes_out);
+/* GetMerklePath for q leaf indices (uint64): paths q x depth x 32 bytes, bits q x depth bytes.
+ * An index >= n yields zero digests and bits 0xff.  Device form reads nodes from
+ * dm_tree_levels_device_async; host form builds the levels itself. */
+int dm_merkle_paths_device_async(dm_ctx *ctx, const void *dev_leaves, const void *dev_nodes, uint64_t n,
+                                 const void *dev_idx, uint64_t q, void *dev_paths, void *dev_bits, void *stream);
+int dm_merkle_paths(dm_ctx *ctx, const uint8_t *leaf_digests, uint64_t n, const uint64_t *idx, uint64_t q,
+                    uint8_t *paths, uint8_t *bits);
+/* Verify q proofs: ok[t] = 1 when SHA-256(content t) folded with path t (depth steps, bits as
+ * above) equals root t.  Roots advance root_stride bytes per proof (0: one shared root; host form:
+ * 0 or 32).  Contents are device pointers (host array) / host chunks. */
+int dm_verify_paths_device_async(dm_ctx *ctx, const void *const *dev_contents, const uint64_t *lens, uint64_t q,
+                                 const void *dev_paths, const void *dev_bits, uint32_t depth, const void *dev_roots,
+                                 uint64_t root_stride, void *dev_ok, void *stream);
+int dm_verify_paths(dm_ctx *ctx, const void *const *contents, const uint64_t *lens, uint64_t q, const uint8_t *paths,
+                    const uint8_t *bits, uint32_t depth, const uint8_t *roots, uint64_t root_stride, uint8_t *ok);
+
 /* ---- tuning ------------------------------------------------------------------------------ */
 
 /* Leaf-kernel selection for uniform-chunk objects (results are identical in every mode):

@@ -25,6 +25,12 @@ Reed-Solomon fragment coding (``py_rs_*`` and ``Oracle.rs_*`` over ``oracle/rs_o
 (``node/tracker.go:250,369``): GF(2^8) mod x^8+x^4+x^3+x^2+1, Vandermonde matrix times the
 inverse of its top square, parity = matrix rows x data shards.  The Python restatement below
 multiplies bitwise (no log tables) so the two restatements share no tables.
+
+FullProcessing (``py_full_processing`` and ``Oracle.full_processing`` over
+``oracle/process_oracle.c``): cess-go-sdk ``process.FullProcessing(file, "", savedir)``
+(``go.mod:8``; not vendored, restated -- composition parity unpinned, see process_oracle.c):
+32 MiB zero-padded segments, RS 4+8 fragments per segment, every segment / fragment named by
+its SHA-256, fid = the hashtree root over the segments.
 """
 from __future__ import annotations
 
@@ -84,6 +90,69 @@ def py_go_tree(chunks: Sequence[bytes]) -> Tuple[List[bytes], bytes]:
             if len(nl) == 2:
                 return leafs, h
         nl = nodes
+
+
+class _GoNode:
+    """merkletree v0.2.0 Node: Parent / Left / Right / Hash / leaf / dup / C."""
+    __slots__ = ("Parent", "Left", "Right", "Hash", "leaf", "dup", "C")
+
+    def __init__(self, Hash, leaf=False, dup=False, C=None, Left=None, Right=None):
+        self.Parent, self.Left, self.Right = None, Left, Right
+        self.Hash, self.leaf, self.dup, self.C = Hash, leaf, dup, C
+
+
+def py_go_tree_nodes(chunks: Sequence[bytes]) -> Tuple[List["_GoNode"], "_GoNode"]:
+    """Literal merkletree v0.2.0 NewTree with Node objects and Parent pointers
+    (buildWithContent + buildIntermediate), for GetMerklePath / VerifyContent restatements."""
+    if len(chunks) == 0:
+        raise ValueError("Empty data")
+    leafs = [_GoNode(py_sha256(c), leaf=True, C=bytes(c)) for c in chunks]
+    if len(leafs) % 2 == 1:
+        last = leafs[-1]
+        leafs.append(_GoNode(last.Hash, leaf=True, dup=True, C=last.C))
+    nl = list(leafs)
+    while True:
+        nodes = []
+        for i in range(0, len(nl), 2):
+            left, right = i, i + 1
+            if i + 1 == len(nl):
+                right = i
+            n = _GoNode(py_sha256(nl[left].Hash + nl[right].Hash), Left=nl[left], Right=nl[right])
+            nodes.append(n)
+            nl[left].Parent = n
+            nl[right].Parent = n
+            if len(nl) == 2:
+                return leafs, n
+        nl = nodes
+
+
+def py_get_merkle_path(chunks: Sequence[bytes], content: bytes) -> Tuple[Optional[List[bytes]], Optional[List[int]]]:
+    """merkletree v0.2.0 GetMerklePath(content): first leaf whose content Equals (HashTreeContent
+    compares strings, hashtree.go:33-35), then up the Parent chain; index 1 when
+    bytes.Equal(parent.Left.Hash, current.Hash) (sibling = Right), else 0 (sibling = Left)."""
+    leafs, _ = py_go_tree_nodes(chunks)
+    for cur in leafs:
+        if cur.C == bytes(content):
+            path, index = [], []
+            parent = cur.Parent
+            while parent is not None:
+                if parent.Left.Hash == cur.Hash:
+                    path.append(parent.Right.Hash)
+                    index.append(1)
+                else:
+                    path.append(parent.Left.Hash)
+                    index.append(0)
+                cur, parent = parent, parent.Parent
+            return path, index
+    return None, None
+
+
+def py_fold_path(leaf_digest: bytes, path: Sequence[bytes], index: Sequence[int]) -> bytes:
+    """Root implied by a GetMerklePath proof: H(h || sib) for index 1, H(sib || h) for index 0."""
+    h = leaf_digest
+    for sib, b in zip(path, index):
+        h = py_sha256(h + sib) if b == 1 else py_sha256(sib + h)
+    return h
 
 
 def py_root_chunks(chunks: Sequence[bytes]) -> Tuple[List[bytes], bytes]:
@@ -203,6 +272,27 @@ def py_rs_encode(data_shards: Sequence[bytes], parity: int) -> List[bytes]:
     return py_rs_code(m[k:], data_shards)
 
 
+def py_full_processing(buf: bytes, segment: int, data: int = 4, parity: int = 8
+                       ) -> Tuple[List[bytes], List[List[bytes]], bytes, List[List[bytes]]]:
+    """FullProcessing restated over hashlib + the bitwise RS restatement.
+
+    Returns (segment digests, per-segment fragment digests (data first), fid, fragments)."""
+    if len(buf) == 0:
+        raise ValueError("empty file")
+    nseg = (len(buf) + segment - 1) // segment
+    padded = bytes(buf) + bytes(nseg * segment - len(buf))
+    segs, frag_h, frags = [], [], []
+    for s in range(nseg):
+        seg = padded[s * segment:(s + 1) * segment]
+        segs.append(py_sha256(seg))
+        dshards = py_rs_split(seg, data)
+        shards = list(dshards) + py_rs_encode(dshards, parity)
+        frags.append(shards)
+        frag_h.append([py_sha256(x) for x in shards])
+    fid = py_reduce(segs)[0]   # NewHashTree(segment paths).MerkleRoot()
+    return segs, frag_h, fid, frags
+
+
 class Oracle:
     """ctypes binding of oracle/merkle_oracle.c and oracle/rs_oracle.c."""
 
@@ -223,6 +313,8 @@ class Oracle:
                                    ctypes.c_size_t, ctypes.c_int]
         L.or_rs_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), vp, ctypes.c_size_t,
                                         ctypes.c_int]
+        L.or_full_processing.argtypes = [vp, u64, u64, ctypes.c_int, ctypes.c_int, vp, vp, vp, vp, ctypes.c_int]
+        L.or_full_processing.restype = ctypes.c_int64
         self.L = L
 
     def backend(self) -> str:
@@ -321,3 +413,26 @@ class Oracle:
         if rc != 0:
             raise ValueError("or_rs_reconstruct failed")
         return [b.raw[:shard] for b in bufs]
+
+    # -- FullProcessing (oracle/process_oracle.c) ----------------------------------------------
+    def full_processing_ptr(self, addr: int, length: int, segment: int, data: int = 4, parity: int = 8,
+                            want_frags: bool = False, nthreads: int = 1):
+        """Returns (segment digests bytes, fragment digests bytes, fid, fragments bytes or None)."""
+        nseg = (length + segment - 1) // segment if length else 0
+        total = data + parity
+        seg = ctypes.create_string_buffer(max(32 * nseg, 32))
+        frag = ctypes.create_string_buffer(max(32 * nseg * total, 32))
+        fid = ctypes.create_string_buffer(32)
+        fr = ctypes.create_string_buffer(nseg * total * (segment // data)) if want_frags else None
+        rc = self.L.or_full_processing(ctypes.c_void_p(addr), length, segment, data, parity, seg, frag, fid, fr,
+                                       nthreads)
+        if rc == -1:
+            raise ValueError("empty file")
+        if rc < 0:
+            raise ValueError(f"or_full_processing rc={rc}")
+        return seg.raw[:32 * nseg], frag.raw[:32 * nseg * total], fid.raw, (fr.raw if fr is not None else None)
+
+    def full_processing(self, buf: bytes, segment: int, data: int = 4, parity: int = 8, want_frags: bool = False,
+                        nthreads: int = 1):
+        b = ctypes.create_string_buffer(bytes(buf), max(len(buf), 1))
+        return self.full_processing_ptr(ctypes.addressof(b), len(buf), segment, data, parity, want_frags, nthreads)

@@ -1,0 +1,245 @@
+"""GPU parity of FullProcessing (dm_process_*) and Merkle proofs (dm_tree_*, dm_merkle_paths*,
+dm_verify_paths*) against the CPU restatements.
+
+Bit-exact against oracle/process_oracle.c and the fixtures in tests/golden/process_golden.json
+(FullProcessing composition parity-unpinned against the SDK itself: see test_process_oracle.py),
+at full segment size (32 MiB segments, 4 + 8 fragments of 8 MiB) through the device-resident form,
+and through the Python mirror of FullProcessing(file, cipher, savedir) writing fragment files.
+Proofs: every fixture path, tree levels for n = 1..300, batched verification of valid and
+tampered proofs, and the hashtree mirror's GetMerklePath / VerifyContent / VerifyTree.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "process_golden.json")
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def pg():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def _processor(ctx, k=4, m=8, segment=32 << 20):
+    from deoss_amd.process import Processor
+    return Processor(ctx, k, m, segment)
+
+
+# ---- FullProcessing ----------------------------------------------------------------------------
+
+def test_process_golden_host(ctx, pg):
+    from oracle import splitmix64_bytes
+    for c in pg["process"]:
+        p = _processor(ctx, c["data"], c["parity"], c["segment"])
+        buf = splitmix64_bytes(c["len"], c["seed"])
+        seg, frag, fid, frags = p.process_buffer(buf, want_frags=True)
+        total = c["data"] + c["parity"]
+        nseg = len(c["segment_hashes"])
+        assert [seg[32 * i:32 * i + 32].hex() for i in range(nseg)] == c["segment_hashes"]
+        assert [[frag[32 * (s * total + j):32 * (s * total + j + 1)].hex() for j in range(total)]
+                for s in range(nseg)] == c["fragment_hashes"]
+        assert fid.hex() == c["fid"]
+        fsz = c["segment"] // c["data"]
+        for t in range(nseg * total):   # fragment bytes hash to their names
+            assert hashlib.sha256(frags[t * fsz:(t + 1) * fsz]).digest() == frag[32 * t:32 * t + 32]
+        p.close()
+
+
+@pytest.mark.parametrize("nbytes", [1, (32 << 20) - 1, 32 << 20, (32 << 20) + 17, 9 * (32 << 20) + 12345])
+def test_process_device_full_segments(ctx, oracle_lib, nbytes):
+    """32 MiB segments, 4 + 8 fragments of 8 MiB, device-resident; stale bytes in the padding
+    region must be zeroed by the call."""
+    torch = _torch()
+    p = _processor(ctx)
+    seg, k, m = 32 << 20, 4, 8
+    nseg = -(-nbytes // seg)
+    obj = torch.full((nseg * seg,), 0xA5, dtype=torch.uint8, device="cuda")
+    p.ctx.fill_synthetic_async(obj.data_ptr(), 0, nbytes // 8 * 8, 0xDE0552000 + nbytes)
+    torch.cuda.synchronize()
+    host = obj[:nbytes].cpu().numpy().tobytes()
+    parity = torch.empty(nseg * m * (seg // k), dtype=torch.uint8, device="cuda")
+    segh = torch.empty(nseg * 32, dtype=torch.uint8, device="cuda")
+    fragh = torch.empty(nseg * (k + m) * 32, dtype=torch.uint8, device="cuda")
+    fid = torch.empty(32, dtype=torch.uint8, device="cuda")
+    p.process_device_async(obj.data_ptr(), nbytes, parity.data_ptr(), segh.data_ptr(), fragh.data_ptr(),
+                           fid.data_ptr())
+    torch.cuda.synchronize()
+    want_seg, want_frag, want_fid, _ = oracle_lib.full_processing(host, seg, k, m, nthreads=8)
+    assert segh.cpu().numpy().tobytes() == want_seg
+    assert fragh.cpu().numpy().tobytes() == want_frag
+    assert fid.cpu().numpy().tobytes() == want_fid
+    if nseg * seg > nbytes:
+        assert int(obj[nbytes:].sum().item()) == 0
+    p.close()
+
+
+def test_process_errors(ctx):
+    from deoss_amd import DeossMerkleError
+    p = _processor(ctx, 4, 8, 64)
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        p.process_buffer(b"")
+    q = _processor(ctx, 4, 8, 100)   # not a multiple of 16 x 4
+    with pytest.raises(DeossMerkleError, match="segment size"):
+        q.process_buffer(b"x" * 10)
+    p.close()
+    q.close()
+
+
+def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch):
+    """FullProcessing(file, "", savedir): fragment files named by their SHA-256, fid = oracle fid;
+    several GPU windows (the fid then comes from dm_tree_levels over all segment digests)."""
+    import deoss_amd.process as proc
+    from oracle import splitmix64_bytes
+    monkeypatch.setattr(proc, "WINDOW_SEGMENTS", 3)
+    p = _processor(ctx, 4, 8, 4096)
+    data = splitmix64_bytes(10 * 4096 + 999, 0xDE0552100)
+    f = tmp_path / "object.bin"
+    f.write_bytes(data)
+    savedir = tmp_path / "cache"
+    info, fid, err = p.FullProcessing(str(f), "", str(savedir))
+    assert err is None
+    seg_b, frag_b, want_fid, frags = oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
+    assert fid == want_fid.hex()
+    assert len(info) == 11
+    for s, si in enumerate(info):
+        assert os.path.basename(si.SegmentHash) == seg_b[32 * s:32 * s + 32].hex()
+        assert len(si.FragmentHash) == 12
+        for j, path in enumerate(si.FragmentHash):
+            t = s * 12 + j
+            assert os.path.basename(path) == frag_b[32 * t:32 * t + 32].hex()
+            assert open(path, "rb").read() == frags[t * 1024:(t + 1) * 1024]
+    # errors keep the Go shape: (nil, "", err)
+    assert p.FullProcessing(str(f), "key", str(savedir))[2] is not None
+    empty = tmp_path / "empty.bin"
+    empty.write_bytes(b"")
+    assert str(p.FullProcessing(str(empty), "", str(savedir))[2]) == "Empty data"
+    assert p.FullProcessing(str(tmp_path / "missing"), "", str(savedir))[2] is not None
+    p.close()
+
+
+# ---- Merkle proofs -----------------------------------------------------------------------------
+
+def test_proof_golden_paths(ctx, pg):
+    for case in pg["proofs"]:
+        leaves = b"".join(bytes.fromhex(h) for h in case["leaves"])
+        # GetMerklePath(content) answers for the first leaf holding that content (it scans Leafs)
+        first = [case["leaves"].index(case["leaves"][p["leaf"]]) for p in case["paths"]]
+        got = ctx.merkle_paths(leaves, first)
+        assert ctx.tree_root(leaves).hex() == case["root"]
+        for (path, bits), p in zip(got, case["paths"]):
+            assert [x.hex() for x in path] == p["path"] and bits == p["index"]
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 17, 100, 255, 256, 257, 300, 513, 1025])
+def test_tree_levels_match_oracle(ctx, n):
+    from oracle import py_level
+    rng = random.Random(n)
+    leaves = [rng.randbytes(32) for _ in range(n)]
+    got = ctx.tree_levels(b"".join(leaves))
+    want, lev = [], leaves
+    while True:
+        lev = py_level(lev)
+        want += lev
+        if len(lev) == 1:
+            break
+    assert got == b"".join(want)
+    assert ctx.tree_node_count(n) == len(want)
+
+
+def test_verify_paths_valid_and_tampered(ctx):
+    from oracle import py_root_chunks
+    rng = random.Random(7)
+    chunks = [rng.randbytes(rng.randrange(0, 3000)) for _ in range(333)]
+    leaves, root = py_root_chunks(chunks)
+    paths = ctx.merkle_paths(b"".join(leaves), list(range(333)))
+    contents = list(chunks)
+    ok = ctx.verify_paths(contents, [p for p, _ in paths], [b for _, b in paths], [root])
+    assert all(ok)
+    contents[5] = contents[5] + b"x"
+    bad_paths = [list(p) for p, _ in paths]
+    bad_paths[9][3] = bytes(32)
+    bad_bits = [list(b) for _, b in paths]
+    bad_bits[11][0] ^= 1
+    bad_bits[12][1] = 2
+    ok = ctx.verify_paths(contents, bad_paths, bad_bits, [root])
+    assert [i for i, v in enumerate(ok) if not v] == [5, 9, 11, 12]
+    # per-proof roots
+    ok = ctx.verify_paths(chunks[:3], [p for p, _ in paths[:3]], [b for _, b in paths[:3]],
+                          [root, bytes(32), root])
+    assert ok == [True, False, True]
+
+
+def test_proofs_device_large(ctx, oracle_lib):
+    """2^17 + 3 leaves of 4 KiB on the device: levels, every path, every proof verified."""
+    torch = _torch()
+    n, chunk = (1 << 17) + 3, 4096
+    obj = torch.empty(n * chunk, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic_async(obj.data_ptr(), 0, n * chunk, 0xDE0552200)
+    leaves = torch.empty(n * 32, dtype=torch.uint8, device="cuda")
+    root = torch.empty(32, dtype=torch.uint8, device="cuda")
+    ctx.root_device_async(obj.data_ptr(), n * chunk, chunk, root.data_ptr(), leaves.data_ptr())
+    nodes = torch.empty(ctx.tree_node_count(n) * 32, dtype=torch.uint8, device="cuda")
+    ctx.tree_levels_device_async(leaves.data_ptr(), n, nodes.data_ptr())
+    depth = ctx.tree_depth(n)
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    paths = torch.empty(n * depth * 32, dtype=torch.uint8, device="cuda")
+    bits = torch.empty(n * depth, dtype=torch.uint8, device="cuda")
+    ctx.merkle_paths_device_async(leaves.data_ptr(), nodes.data_ptr(), n, idx.data_ptr(), n, paths.data_ptr(),
+                                  bits.data_ptr())
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    base = obj.data_ptr()
+    ctx.verify_paths_device_async([base + i * chunk for i in range(n)], [chunk] * n, n, paths.data_ptr(),
+                                  bits.data_ptr(), depth, root.data_ptr(), 0, ok.data_ptr())
+    torch.cuda.synchronize()
+    assert int(ok.sum().item()) == n
+    assert nodes[-32:].cpu().numpy().tobytes() == root.cpu().numpy().tobytes()
+    host = obj.cpu().numpy().tobytes()
+    _, want_root = oracle_lib.root_buffer(host, chunk, nthreads=8)
+    assert root.cpu().numpy().tobytes() == want_root
+    # one tampered byte fails exactly its own proof
+    obj[77 * chunk + 5] ^= 1
+    ok.zero_()
+    ctx.verify_paths_device_async([base + i * chunk for i in range(n)], [chunk] * n, n, paths.data_ptr(),
+                                  bits.data_ptr(), depth, root.data_ptr(), 0, ok.data_ptr())
+    torch.cuda.synchronize()
+    bad = torch.nonzero(ok == 0).flatten().cpu().tolist()
+    assert bad == [77]
+
+
+def test_hashtree_mirror_proof_api(ctx, tmp_path):
+    from deoss_amd import HashTreeContent, NewHashTree
+    from oracle import py_fold_path, py_get_merkle_path
+    contents = [b"content_one", b"content_two", b"content_three", b"content_two", b"content_five"]
+    paths = []
+    for i, c in enumerate(contents):
+        p = tmp_path / f"c{i}"
+        p.write_bytes(c)
+        paths.append(str(p))
+    tree, err = NewHashTree(paths, ctx=ctx, keep_content=True)
+    assert err is None
+    for c in contents:
+        path, index, err = tree.GetMerklePath(HashTreeContent(c))
+        assert err is None
+        assert (path, index) == py_get_merkle_path(contents, c)
+        assert py_fold_path(hashlib.sha256(c).digest(), path, index) == tree.MerkleRoot()
+        ok, err = tree.VerifyContent(HashTreeContent(c))
+        assert ok and err is None
+    assert tree.GetMerklePath(HashTreeContent(b"absent")) == (None, None, None)
+    assert tree.VerifyContent(HashTreeContent(b"absent")) == (False, None)
+    assert tree.VerifyTree() == (True, None)
+    tree.Leafs[2].C.x = b"tampered"
+    assert tree.VerifyTree() == (False, None)
