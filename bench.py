@@ -566,15 +566,11 @@ def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
                                   bits.data_ptr(), sptr)
     torch.cuda.synchronize()
     t_paths = time.perf_counter() - t0
-    base = obj.data_ptr()
-    ptrs = [base + i * leaf for i in range(n)]
-    lens = [leaf] * n
-
     def step():
-        ctx.verify_paths_device_async(ptrs, lens, n, paths.data_ptr(), bits.data_ptr(), depth, root.data_ptr(), 0,
-                                      ok.data_ptr(), sptr)
+        ctx.verify_object_device_async(obj.data_ptr(), n * leaf, leaf, paths.data_ptr(), bits.data_ptr(), depth,
+                                       root.data_ptr(), 0, ok.data_ptr(), sptr)
 
-    elapsed, calls, _, _ = timed_steps(args, torch, dist, world, device, gloo, ctx, step)
+    elapsed, calls, k_sum, call_sum = timed_steps(args, torch, dist, world, device, gloo, ctx, step)
     all_ok = int(ok.sum().item()) == n
     orc = Oracle()
     host = obj.cpu().numpy()
@@ -591,6 +587,8 @@ def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
         "config": {"workload": f"{n} leaves x {leaf} B, depth {depth}, every leaf's proof per step",
                    "leaves": n, "leaf_bytes": leaf, "depth": depth},
         "levels_ms": round(t_levels * 1e3, 3), "paths_ms": round(t_paths * 1e3, 3),
+        "leaf_kernel_avg_ms": round(k_sum / max(calls, 1), 3), "call_avg_ms": round(call_sum / max(calls, 1), 3),
+        "leaf_kernel": ctx.leaf_kernel_for(n),
         "content_GiBps": round(n * leaf * world * args.steps / elapsed / (1 << 30), 3),
         "parity": {"all_proofs_verify": all_ok, "root_matches_cpu": root_ok, "bit_exact": all_ok and root_ok},
     }

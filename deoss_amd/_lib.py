@@ -38,6 +38,7 @@ EXPORTS = (
     "dm_process_device_async", "dm_process_buffer",
     "dm_tree_node_count", "dm_tree_depth", "dm_tree_levels_device_async", "dm_tree_levels",
     "dm_merkle_paths_device_async", "dm_merkle_paths", "dm_verify_paths_device_async", "dm_verify_paths",
+    "dm_verify_object_device_async",
 )
 
 
@@ -99,6 +100,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_merkle_paths": ([vp, vp, u64, vp, u64, vp, vp], i32),
         "dm_verify_paths_device_async": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
         "dm_verify_paths": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp], i32),
+        "dm_verify_object_device_async": ([vp, vp, u64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -79,6 +79,27 @@ int verify_dev(dm_ctx* c, Dev& d, hipStream_t s, const void* const* contents, co
     return DM_OK;
 }
 
+// Uniform layout: the n chunks of one object (leaf i at dev + i * chunk, the last one short).
+int verify_object_dev(dm_ctx* c, Dev& d, hipStream_t s, const void* dev, uint64_t len, uint64_t chunk,
+                      const uint8_t* paths, const uint8_t* bits, uint32_t depth, const uint8_t* roots,
+                      uint64_t root_stride, uint8_t* ok) {
+    dm::LeafArgs la = uniform_args(dev, len, chunk);
+    const uint64_t q = la.nleaves;
+    HIP_TRY(d.leaves.ensure(q * 32));
+    la.byte_end = ~0ull;
+    la.digests = d.leaves.u8();
+    const bool aligned = is_aligned16(dev) && chunk % 16 == 0;
+    hipEvent_t* tr = timing_record(c, d);
+    if (tr) HIP_TRY(hipEventRecord(tr[0], s));
+    RC_TRY(launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, q)));
+    if (tr) HIP_TRY(hipEventRecord(tr[1], s));
+    hipLaunchKernelGGL(dm::verify_kernel, dim3((uint32_t)ceil_div(q, dm::kProofBlock)), dim3(dm::kProofBlock), 0, s,
+                       d.leaves.u8(), paths, bits, depth, q, roots, root_stride, ok);
+    HIP_TRY(hipGetLastError());
+    if (tr) HIP_TRY(hipEventRecord(tr[2], s));
+    return DM_OK;
+}
+
 bool aligned_all(std::initializer_list<const void*> ps) {
     for (const void* p : ps)
         if (!p || !is_aligned16(p)) return false;
@@ -189,6 +210,24 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
     return verify_dev(c, d, s, dev_contents, lens, q, static_cast<const uint8_t*>(dev_paths),
                       static_cast<const uint8_t*>(dev_bits), depth, static_cast<const uint8_t*>(dev_roots),
                       root_stride, static_cast<uint8_t*>(dev_ok));
+}
+
+int dm_verify_object_device_async(dm_ctx* ctx, const void* dev_obj, uint64_t len, uint64_t chunk,
+                                  const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
+                                  uint64_t root_stride, void* dev_ok, void* stream) {
+    if (!ctx) return DM_ERR_INVALID;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    dm_ctx* c = ctx;
+    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    if (chunk == 0 || !dev_obj || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
+        root_stride % 16)
+        return fail(c, DM_ERR_INVALID, "dm_verify_object_device_async: null or misaligned argument, or depth 0");
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    return verify_object_dev(c, d, s, dev_obj, len, chunk, static_cast<const uint8_t*>(dev_paths),
+                             static_cast<const uint8_t*>(dev_bits), depth, static_cast<const uint8_t*>(dev_roots),
+                             root_stride, static_cast<uint8_t*>(dev_ok));
 }
 
 int dm_verify_paths(dm_ctx* ctx, const void* const* contents, const uint64_t* lens, uint64_t q, const uint8_t* paths,

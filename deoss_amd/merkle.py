@@ -246,6 +246,15 @@ class MerkleContext:
                                                          ctypes.c_void_p(stream or None)),
                     "dm_verify_paths_device_async")
 
+    def verify_object_device_async(self, dev_obj: int, length: int, chunk: int, dev_paths: int, dev_bits: int,
+                                   depth: int, dev_roots: int, root_stride: int, dev_ok: int, stream: int = 0) -> None:
+        """Every chunk of one object in HBM against its proof (uniform layout, no tables)."""
+        self._check(self._L.dm_verify_object_device_async(self._h, ctypes.c_void_p(dev_obj), length, chunk,
+                                                          ctypes.c_void_p(dev_paths), ctypes.c_void_p(dev_bits), depth,
+                                                          ctypes.c_void_p(dev_roots), root_stride,
+                                                          ctypes.c_void_p(dev_ok), ctypes.c_void_p(stream or None)),
+                    "dm_verify_object_device_async")
+
     # -- streaming -------------------------------------------------------------------------------
     def open_stream(self, chunk: int) -> "MerkleStream":
         """Incremental root of one object written in pieces (hash while receiving)."""

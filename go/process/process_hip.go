@@ -1,0 +1,145 @@
+//go:build hip
+
+// Package process is a GPU-backed stand-in for cess-go-sdk core/process.FullProcessing (DeOSS
+// go.mod:8), the call every upload handler makes to get the file id and the fragment names
+// (node/objectHandler.go:168, node/fileHandler.go:771, node/filesHandler.go:201,
+// node/resumeHandler.go:326, node/tracker.go:767-769) and the fragment download path re-runs
+// (node/fileHandler.go:964,997).  Same signature and result shape; segmenting, Reed-Solomon 4 + 8
+// coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h,
+// dm_process_buffer and dm_tree_levels).  Swap it in by changing the handlers' import of
+// github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
+// Deviations: cipher must be "" (the AES branch is not implemented), and segment files are not
+// written (their bytes are the data fragments in order).  Build with `-tags hip`, CGO_ENABLED=1.
+package process
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../deoss_amd -ldeoss_merkle -Wl,-rpath,${SRCDIR}/../../deoss_amd
+#include <stdlib.h>
+#include "deoss_merkle.h"
+*/
+import "C"
+
+import (
+	"encoding/hex"
+	"errors"
+	"io"
+	"os"
+	"path/filepath"
+	"sync"
+	"unsafe"
+
+	"github.com/CESSProject/cess-go-sdk/chain"
+)
+
+// windowSegments is the number of segments coded per GPU call (2 GiB of file at 32 MiB).
+const windowSegments = 64
+
+var (
+	once   sync.Once
+	ctx    *C.dm_ctx
+	rs     *C.dm_rs
+	initEr error
+	mu     sync.Mutex // dm_rs calls serialise on the context anyway; keeps buffers per call simple
+)
+
+func gpu() error {
+	once.Do(func() {
+		if rc := C.dm_create(&ctx, nil, 0); rc != C.DM_OK {
+			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
+			return
+		}
+		if rc := C.dm_rs_create(ctx, C.int(chain.DataShards), C.int(chain.ParShards), &rs); rc != C.DM_OK {
+			initEr = errors.New(C.GoString(C.dm_last_error(ctx)))
+		}
+	})
+	return initEr
+}
+
+func rcError(rc C.int) error {
+	if rc == C.DM_ERR_EMPTY {
+		return errors.New("Empty data")
+	}
+	if msg := C.GoString(C.dm_last_error(ctx)); msg != "" {
+		return errors.New(msg)
+	}
+	return errors.New(C.GoString(C.dm_strerror(rc)))
+}
+
+// FullProcessing cuts file into chain.SegmentSize segments (the last zero-padded), codes each into
+// chain.DataShards + chain.ParShards fragments written to savedir/<hex SHA-256>, and returns the
+// segment / fragment path names and the fid (hex hashtree root over the segments).
+func FullProcessing(file string, cipher string, savedir string) ([]chain.SegmentDataInfo, string, error) {
+	if cipher != "" {
+		return nil, "", errors.New("process: cipher is not supported by the GPU pipeline")
+	}
+	if err := gpu(); err != nil {
+		return nil, "", err
+	}
+	f, err := os.Open(file)
+	if err != nil {
+		return nil, "", err
+	}
+	defer f.Close()
+	if err = os.MkdirAll(savedir, 0755); err != nil {
+		return nil, "", err
+	}
+	seg := uint64(chain.SegmentSize)
+	total := chain.DataShards + chain.ParShards
+	frag := seg / uint64(chain.DataShards)
+	window := make([]byte, windowSegments*seg)
+	var info []chain.SegmentDataInfo
+	var segDigests []byte
+	var fid [32]byte
+	mu.Lock()
+	defer mu.Unlock()
+	for {
+		n, rerr := io.ReadFull(f, window)
+		if n == 0 {
+			if rerr == io.EOF && len(info) == 0 {
+				return nil, "", errors.New("Empty data")
+			}
+			break
+		}
+		nseg := (uint64(n) + seg - 1) / seg
+		frags := make([]byte, nseg*uint64(total)*frag)
+		segd := make([]byte, 32*nseg)
+		fragd := make([]byte, 32*nseg*uint64(total))
+		rc := C.dm_process_buffer(rs, unsafe.Pointer(&window[0]), C.uint64_t(n), C.uint64_t(seg),
+			unsafe.Pointer(&frags[0]), (*C.uint8_t)(unsafe.Pointer(&segd[0])),
+			(*C.uint8_t)(unsafe.Pointer(&fragd[0])), (*C.uint8_t)(unsafe.Pointer(&fid[0])))
+		if rc != C.DM_OK {
+			return nil, "", rcError(rc)
+		}
+		for s := uint64(0); s < nseg; s++ {
+			names := make([]string, total)
+			for j := 0; j < total; j++ {
+				t := s*uint64(total) + uint64(j)
+				p := filepath.Join(savedir, hex.EncodeToString(fragd[32*t:32*t+32]))
+				if _, err := os.Stat(p); err != nil {
+					if err = os.WriteFile(p, frags[t*frag:(t+1)*frag], os.ModePerm); err != nil {
+						return nil, "", err
+					}
+				}
+				names[j] = p
+			}
+			info = append(info, chain.SegmentDataInfo{
+				SegmentHash:  filepath.Join(savedir, hex.EncodeToString(segd[32*s:32*s+32])),
+				FragmentHash: names,
+			})
+		}
+		segDigests = append(segDigests, segd...)
+		if rerr != nil { // short final window
+			break
+		}
+	}
+	if len(info) > windowSegments { // several windows: the fid is the tree over every segment
+		nodes := make([]byte, 32*uint64(C.dm_tree_node_count(C.uint64_t(len(info)))))
+		if rc := C.dm_tree_levels(ctx, (*C.uint8_t)(unsafe.Pointer(&segDigests[0])), C.uint64_t(len(info)),
+			(*C.uint8_t)(unsafe.Pointer(&nodes[0]))); rc != C.DM_OK {
+			return nil, "", rcError(rc)
+		}
+		copy(fid[:], nodes[len(nodes)-32:])
+	}
+	return info, hex.EncodeToString(fid[:]), nil
+}

@@ -208,6 +208,11 @@ int dm_merkle_paths(dm_ctx *ctx, const uint8_t *leaf_digests, uint64_t n, const 
 int dm_verify_paths_device_async(dm_ctx *ctx, const void *const *dev_contents, const uint64_t *lens, uint64_t q,
                                  const void *dev_paths, const void *dev_bits, uint32_t depth, const void *dev_roots,
                                  uint64_t root_stride, void *dev_ok, void *stream);
+/* Uniform form: the ceil(len / chunk) chunks of one object in HBM (chunk i at dev_obj + i * chunk,
+ * the last one short) checked against proofs t = 0 .. n-1 -- no per-content table. */
+int dm_verify_object_device_async(dm_ctx *ctx, const void *dev_obj, uint64_t len, uint64_t chunk,
+                                  const void *dev_paths, const void *dev_bits, uint32_t depth, const void *dev_roots,
+                                  uint64_t root_stride, void *dev_ok, void *stream);
 int dm_verify_paths(dm_ctx *ctx, const void *const *contents, const uint64_t *lens, uint64_t q, const uint8_t *paths,
                     const uint8_t *bits, uint32_t depth, const uint8_t *roots, uint64_t root_stride, uint8_t *ok);
 

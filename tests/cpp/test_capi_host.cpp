@@ -22,6 +22,10 @@ int or_root_chunks(const void* const* ptrs, const uint64_t* lens, uint64_t n, ui
 void or_fill_splitmix(void* dst, uint64_t off, uint64_t nbytes, uint64_t seed);
 int or_rs_encode(int data, int parity, const uint8_t* const* dshards, uint8_t* const* pshards, size_t shard,
                  int nthreads);
+int64_t or_full_processing(const void* buf, uint64_t len, uint64_t segment, int data, int parity,
+                           uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t fid[32], uint8_t* frags, int nthreads);
+uint64_t or_reduce(const uint8_t* digests, uint64_t n, int levels, uint8_t* out);
+void or_sha256(const void* data, uint64_t len, uint8_t out[32]);
 }
 
 static int fails = 0;
@@ -251,6 +255,87 @@ int main() {
         (void)hipFree(dd);
         (void)hipFree(dpar);
         dm_rs_destroy(rs);
+    }
+
+    // FullProcessing: host and device forms vs the oracle (small segments, 4 + 8)
+    {
+        dm_rs* rs = nullptr;
+        EXPECT(dm_rs_create(c, 4, 8, &rs) == DM_OK);
+        const uint64_t seg = 4096, frag = seg / 4;
+        for (uint64_t len : {1ull, 4096ull, 4097ull, 50000ull}) {
+            const uint64_t nseg = (len + seg - 1) / seg;
+            auto obj = bytes(len, 31337 + len);
+            std::vector<uint8_t> ws(32 * nseg), wf(32 * nseg * 12), wfr(nseg * 12 * frag), gs(ws.size()),
+                gf(wf.size()), gfr(wfr.size());
+            uint8_t wfid[32], gfid[32];
+            EXPECT(or_full_processing(obj.data(), len, seg, 4, 8, ws.data(), wf.data(), wfid, wfr.data(), 1) ==
+                   (int64_t)nseg);
+            EXPECT(dm_process_buffer(rs, obj.data(), len, seg, gfr.data(), gs.data(), gf.data(), gfid) == DM_OK);
+            EXPECT(ws == gs && wf == gf && wfr == gfr && std::memcmp(wfid, gfid, 32) == 0);
+            // device form, stale bytes in the padding
+            void *dobj = nullptr, *dpar = nullptr, *dh = nullptr;
+            EXPECT(hipMalloc(&dobj, nseg * seg) == hipSuccess && hipMalloc(&dpar, nseg * 8 * frag) == hipSuccess &&
+                   hipMalloc(&dh, 32 * nseg * 13 + 32) == hipSuccess);
+            EXPECT(hipMemset(dobj, 0x5a, nseg * seg) == hipSuccess);
+            EXPECT(hipMemcpy(dobj, obj.data(), len, hipMemcpyHostToDevice) == hipSuccess);
+            uint8_t* h = static_cast<uint8_t*>(dh);
+            EXPECT(dm_process_device_async(rs, dobj, len, seg, dpar, h, h + 32 * nseg, h + 32 * nseg * 13, nullptr) ==
+                   DM_OK);
+            EXPECT(hipDeviceSynchronize() == hipSuccess);
+            std::vector<uint8_t> back(32 * nseg * 13 + 32);
+            EXPECT(hipMemcpy(back.data(), dh, back.size(), hipMemcpyDeviceToHost) == hipSuccess);
+            EXPECT(std::memcmp(back.data(), ws.data(), ws.size()) == 0);
+            EXPECT(std::memcmp(back.data() + ws.size(), wf.data(), wf.size()) == 0);
+            EXPECT(std::memcmp(back.data() + 32 * nseg * 13, wfid, 32) == 0);
+            (void)hipFree(dobj);
+            (void)hipFree(dpar);
+            (void)hipFree(dh);
+        }
+        uint8_t fid[32];
+        EXPECT(dm_process_buffer(rs, nullptr, 0, seg, nullptr, nullptr, nullptr, fid) == DM_ERR_EMPTY);
+        EXPECT(dm_process_buffer(rs, fid, 1, 100, nullptr, nullptr, nullptr, fid) == DM_ERR_INVALID);
+        dm_rs_destroy(rs);
+    }
+
+    // Merkle proofs: levels, paths, verification (host forms)
+    {
+        const uint64_t n = 1000;
+        std::vector<std::vector<uint8_t>> ct;
+        std::vector<uint8_t> lv(32 * n);
+        for (uint64_t i = 0; i < n; i++) {
+            ct.push_back(bytes(i % 300, 77 + i % 500));   // repeated contents
+            or_sha256(ct.back().data(), ct.back().size(), lv.data() + 32 * i);
+        }
+        EXPECT(dm_tree_node_count(n) == 500 + 250 + 125 + 63 + 32 + 16 + 8 + 4 + 2 + 1);
+        EXPECT(dm_tree_depth(n) == 10 && dm_tree_depth(1) == 1 && dm_tree_depth(2) == 1 && dm_tree_depth(3) == 2);
+        std::vector<uint8_t> nodes(32 * dm_tree_node_count(n));
+        EXPECT(dm_tree_levels(c, lv.data(), n, nodes.data()) == DM_OK);
+        uint8_t want_root[32];
+        or_reduce(lv.data(), n, -1, want_root);
+        EXPECT(std::memcmp(nodes.data() + nodes.size() - 32, want_root, 32) == 0);
+        std::vector<uint64_t> idx(n);
+        for (uint64_t i = 0; i < n; i++) idx[i] = i;
+        const uint32_t D = dm_tree_depth(n);
+        std::vector<uint8_t> paths(32 * D * n), bits(D * n), ok(n);
+        EXPECT(dm_merkle_paths(c, lv.data(), n, idx.data(), n, paths.data(), bits.data()) == DM_OK);
+        std::vector<const void*> cp(n);
+        std::vector<uint64_t> cl(n);
+        for (uint64_t i = 0; i < n; i++) {
+            cp[i] = ct[i].data();
+            cl[i] = ct[i].size();
+        }
+        EXPECT(dm_verify_paths(c, cp.data(), cl.data(), n, paths.data(), bits.data(), D, want_root, 0, ok.data()) ==
+               DM_OK);
+        uint64_t good = 0;
+        for (auto v : ok) good += v;
+        EXPECT(good == n);
+        paths[32 * D * 17 + 5] ^= 1;
+        EXPECT(dm_verify_paths(c, cp.data(), cl.data(), n, paths.data(), bits.data(), D, want_root, 0, ok.data()) ==
+               DM_OK);
+        EXPECT(ok[17] == 0 && ok[16] == 1 && ok[18] == 1);
+        EXPECT(dm_tree_levels(c, lv.data(), 0, nodes.data()) == DM_ERR_EMPTY);
+        EXPECT(dm_verify_paths(c, cp.data(), cl.data(), n, paths.data(), bits.data(), D, want_root, 16, ok.data()) ==
+               DM_ERR_INVALID);
     }
 
     // concurrent callers on one context

@@ -218,6 +218,39 @@ def test_proofs_device_large(ctx, oracle_lib):
     torch.cuda.synchronize()
     bad = torch.nonzero(ok == 0).flatten().cpu().tolist()
     assert bad == [77]
+    # uniform-layout form (no per-content table) gives the same answers
+    ok.fill_(7)
+    ctx.verify_object_device_async(obj.data_ptr(), n * chunk, chunk, paths.data_ptr(), bits.data_ptr(), depth,
+                                   root.data_ptr(), 0, ok.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.nonzero(ok != 1).flatten().cpu().tolist() == [77]
+
+
+@pytest.mark.parametrize("n,chunk,tail", [(1, 64, 0), (2, 64, 1), (3, 4096, 100), (1000, 1000, 7)])
+def test_verify_object_ragged(ctx, n, chunk, tail):
+    """Uniform form with a short last chunk and odd leaf counts, per-proof roots."""
+    torch = _torch()
+    from oracle import py_get_merkle_path, py_root_chunks
+    length = (n - 1) * chunk + (tail or chunk)
+    obj = torch.empty(length + 64, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic_async(obj.data_ptr(), 0, (length + 7) // 8 * 8, 0xDE0552300 + n)
+    host = obj[:length].cpu().numpy().tobytes()
+    chunks = [host[i * chunk:(i + 1) * chunk] for i in range(n)]
+    leaves, root = py_root_chunks(chunks)
+    depth = ctx.tree_depth(n)
+    pb, bb = b"", b""
+    for i in range(n):
+        p, b = py_get_merkle_path(chunks, chunks[i])
+        pb += b"".join(p)
+        bb += bytes(b)
+    paths = torch.frombuffer(bytearray(pb), dtype=torch.uint8).cuda()
+    bits = torch.frombuffer(bytearray(bb), dtype=torch.uint8).cuda()
+    roots = torch.frombuffer(bytearray(root * n), dtype=torch.uint8).cuda()
+    ok = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    ctx.verify_object_device_async(obj.data_ptr(), length, chunk, paths.data_ptr(), bits.data_ptr(), depth,
+                                   roots.data_ptr(), 32, ok.data_ptr())
+    torch.cuda.synchronize()
+    assert int(ok.sum().item()) == n
 
 
 def test_hashtree_mirror_proof_api(ctx, tmp_path):
