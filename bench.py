@@ -77,7 +77,7 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
-    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs", "process", "proofs"],
+    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
                          "upload: one object fed in pieces through dm_stream (hash while receiving)")
@@ -85,6 +85,12 @@ def main() -> None:
     ap.add_argument("--segment-mib", type=int, default=32, help="rs: segment bytes (chain.SegmentSize)")
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
     ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
+    ap.add_argument("--threads", type=int, default=256, help="concurrent: caller threads")
+    ap.add_argument("--mode", default="root", choices=["root", "process"], help="concurrent: request kind")
+    ap.add_argument("--slots", type=int, default=0, help="concurrent: batcher worker slots (0 = library default)")
+    ap.add_argument("--max-leaves", type=int, default=0, help="concurrent: leaf budget per batch (0 = default)")
+    ap.add_argument("--linger-us", type=int, default=2000, help="concurrent: batcher linger after the first request")
+    ap.add_argument("--no-shared", action="store_true", help="concurrent: skip the serialised shared-context timing")
     ap.add_argument("--sweep-chunks", default="4096,65536,1048576,8388608,33554432")
     ap.add_argument("--sweep-modes", action="store_true", help="sweep every leaf kernel (wide, latency, pair, quad)")
     ap.add_argument("--leaf-kernel", default="auto", choices=["auto", "wide", "latency", "pair", "quad"])
@@ -122,6 +128,8 @@ def main() -> None:
         return run_process(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload == "proofs":
         return run_proofs(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "concurrent":
+        return run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload != "object":
         return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
     per_gpu = int(args.object_gib * (1 << 30))
@@ -592,6 +600,123 @@ def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
         "content_GiBps": round(n * leaf * world * args.steps / elapsed / (1 << 30), 3),
         "parity": {"all_proofs_verify": all_ok, "root_matches_cpu": root_ok, "bit_exact": all_ok and root_ok},
     }
+    print(json.dumps(out), flush=True)
+
+
+def run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo):
+    """Upload-gateway regime: --threads caller threads, each blocking on one request at a time
+    (NewHashTreeFromBuffer at --chunk, or FullProcessing at 32 MiB segments), --objects requests of
+    --object-mib each from host memory.  Timed twice: through the coalescing dm_batcher, and
+    through one shared context (what one call per request gives: calls serialise).  Host
+    residency and H2D are inside the timed region."""
+    import threading
+    from deoss_amd import MerkleContext
+    from deoss_amd.batcher import PROCESS as B_PROCESS, ROOT as B_ROOT, Batcher
+    from deoss_amd.process import Processor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    obj = int(args.object_mib * (1 << 20))
+    nreq = args.objects
+    seg = args.segment_mib << 20
+    unit = args.chunk if args.mode == "root" else seg
+    ctx = MerkleContext(devices=[dev_index])
+    pitch = (obj + 4095) // 4096 * 4096
+    dev = torch.empty(pitch * nreq, dtype=torch.uint8, device=device)
+    for j in range(nreq):
+        ctx.fill_synthetic_async(dev.data_ptr() + j * pitch, 0, (obj + 7) // 8 * 8, SEED + 0x400 + j)
+    host = dev.cpu().numpy()
+    del dev
+    base = host.ctypes.data
+    outs = [None] * nreq
+
+    def drive(call, n=nreq):
+        nxt = [0]
+        lock = threading.Lock()
+
+        def worker():
+            while True:
+                with lock:
+                    j = nxt[0]
+                    nxt[0] += 1
+                if j >= n:
+                    return
+                outs[j] = call(j)
+
+        th = [threading.Thread(target=worker) for _ in range(args.threads)]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        return time.perf_counter() - t0
+
+    res = {}
+    if args.mode == "root":
+        b = Batcher(B_ROOT, unit, device=dev_index, slots=args.slots, max_leaves=args.max_leaves,
+                    linger_us=args.linger_us)
+        for _ in range(args.warmup):   # untimed passes: every slot grows its buffers once
+            drive(lambda j: b.root((base + j * pitch, obj))[1])
+        s0 = b.stats()
+        res["batcher"] = drive(lambda j: b.root((base + j * pitch, obj))[1])
+        stats = [x - y for x, y in zip(b.stats(), s0)]
+        stats[2] = b.stats()[2]
+        b.close()
+        got = list(outs)
+        if not args.no_shared:   # serialised: time a sample of requests and scale
+            sample = max(1, min(nreq, 256))
+            res["shared_context"] = drive(lambda j: ctx.root_buffer_ptr(base + j * pitch, obj, unit)[1],
+                                          sample) * nreq / sample
+    else:
+        b = Batcher(B_PROCESS, unit, 4, 8, device=dev_index, slots=args.slots, max_leaves=args.max_leaves,
+                    linger_us=args.linger_us)
+        for _ in range(args.warmup):
+            drive(lambda j: b.process((base + j * pitch, obj))[2])
+        s0 = b.stats()
+        res["batcher"] = drive(lambda j: b.process((base + j * pitch, obj))[2])
+        stats = [x - y for x, y in zip(b.stats(), s0)]
+        stats[2] = b.stats()[2]
+        b.close()
+        got = list(outs)
+        proc = Processor(ctx, 4, 8, unit)
+        import ctypes as _ct
+        sample = max(1, min(nreq, 8))
+
+        def one(j):
+            src = (_ct.c_char * obj).from_address(base + j * pitch)
+            return proc.process_buffer(src, want_frags=False)[2]
+        # the serialised path is slow: time a sample of requests and scale
+        if not args.no_shared:
+            res["shared_context"] = drive(one, sample) * nreq / sample
+    orc = Oracle()
+    mism, check = 0, min(nreq, 256)
+    for j in range(check):
+        addr = base + j * pitch
+        if args.mode == "root":
+            want = orc.root_buffer_ptr(addr, obj, unit, nthreads=4)[1]
+        else:
+            want = orc.full_processing_ptr(addr, obj, unit, 4, 8, nthreads=4)[2]
+        mism += want != got[j]
+    total = obj * nreq
+    out = {
+        "metric": ("host-resident GiB/s of uploads hashed to Merkle roots by concurrent callers" if args.mode == "root"
+                   else "host-resident GiB/s of uploads through FullProcessing by concurrent callers"),
+        "value": round(total / res["batcher"] / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 1,
+        "steps": 1, "warmup": args.warmup, "ms_per_step": round(res["batcher"] * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic splitmix64 objects in host memory",
+        "config": {"workload": f"{nreq} requests x {obj} B from {args.threads} threads, "
+                               f"{'chunk' if args.mode == 'root' else 'segment'} {unit} B ({args.mode})",
+                   "threads": args.threads, "requests": nreq, "object_bytes": obj, "unit": unit},
+        "batcher": {"seconds": round(res["batcher"], 4), "requests": stats[0], "batches": stats[1],
+                    "largest_batch": stats[2], "slots": args.slots or 2, "max_leaves": args.max_leaves or 2048,
+                    "linger_us": args.linger_us},
+        "parity": {"checked": check, "mismatches": int(mism), "bit_exact": mism == 0},
+    }
+    if "shared_context" in res:
+        out["shared_context"] = {"seconds": round(res["shared_context"], 4),
+                                 "GiBps": round(total / res["shared_context"] / (1 << 30), 4),
+                                 "note": "one dm_ctx for all threads: calls serialise (timed on a sample of "
+                                         "256 (root) / 8 (process) requests, scaled)"}
+        out["speedup_vs_shared_context"] = round(res["shared_context"] / res["batcher"], 2)
     print(json.dumps(out), flush=True)
 
 

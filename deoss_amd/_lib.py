@@ -35,10 +35,12 @@ EXPORTS = (
     "dm_timing_summary",
     "dm_rs_create", "dm_rs_destroy", "dm_rs_matrix", "dm_rs_encode", "dm_rs_encode_buffer", "dm_rs_reconstruct",
     "dm_rs_verify", "dm_rs_encode_device_async", "dm_rs_reconstruct_device_async",
-    "dm_process_device_async", "dm_process_buffer",
+    "dm_process_device_async", "dm_process_buffer", "dm_process_batch",
     "dm_tree_node_count", "dm_tree_depth", "dm_tree_levels_device_async", "dm_tree_levels",
     "dm_merkle_paths_device_async", "dm_merkle_paths", "dm_verify_paths_device_async", "dm_verify_paths",
     "dm_verify_object_device_async",
+    "dm_batcher_create", "dm_batcher_destroy", "dm_batcher_root", "dm_batcher_process", "dm_batcher_stats",
+    "dm_batcher_last_error",
 )
 
 
@@ -92,6 +94,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_rs_reconstruct_device_async": ([vp, pvp, vp, u64, vp], i32),
         "dm_process_device_async": ([vp, vp, u64, u64, vp, vp, vp, vp, vp], i32),
         "dm_process_buffer": ([vp, vp, u64, u64, vp, vp, vp, vp], i32),
+        "dm_process_batch": ([vp, pvp, pu64, u64, u64, pvp, pvp, pvp, vp], i32),
         "dm_tree_node_count": ([u64], u64),
         "dm_tree_depth": ([u64], u32),
         "dm_tree_levels_device_async": ([vp, vp, u64, vp, vp], i32),
@@ -101,6 +104,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_verify_paths_device_async": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
         "dm_verify_paths": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp], i32),
         "dm_verify_object_device_async": ([vp, vp, u64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
+        "dm_batcher_create": ([i32, i32, u64, i32, i32, i32, u64, u64, u32, ctypes.POINTER(vp)], i32),
+        "dm_batcher_destroy": ([vp], None),
+        "dm_batcher_root": ([vp, vp, u64, vp, vp], i32),
+        "dm_batcher_process": ([vp, vp, u64, vp, vp, vp, vp], i32),
+        "dm_batcher_stats": ([vp, pu64, pu64, pu64], i32),
+        "dm_batcher_last_error": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -399,19 +399,11 @@ int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, cons
     return DM_OK;
 }
 
-// Pack host chunks into device memory (256-B aligned starts) through the pinned ring.
-// Returns the device address of each chunk in `addr`.
-int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uint64_t n,
-                std::vector<uint64_t>& addr) {
-    std::vector<uint64_t> off(n);
-    uint64_t total = 0;
-    for (uint64_t i = 0; i < n; i++) {
-        off[i] = total;
-        total = round_up(total + lens[i], kAlign);
-    }
-    HIP_TRY(d.data.ensure(std::max<uint64_t>(total, kAlign)));
-    addr.resize(n);
-    for (uint64_t i = 0; i < n; i++) addr[i] = reinterpret_cast<uint64_t>(d.data.u8() + off[i]);
+// Copy host chunks to d.data + off[i] (device offsets chosen by the caller, 256-B aligned,
+// non-overlapping; bytes up to the next 256-B boundary after a chunk may be overwritten) through
+// the pinned ring, or straight from the caller's memory when every chunk is pinned.
+int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uint64_t n,
+           const std::vector<uint64_t>& off) {
     // Pinned sources (every chunk in page-locked host memory): async copies straight from the
     // caller's buffers, coalescing runs that are contiguous on both sides with no padding between
     // them (so a copy never reads a host byte outside the caller's chunks).
@@ -428,7 +420,7 @@ int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens
             if (lens[i] == 0) { i++; continue; }
             const uint8_t* h0 = static_cast<const uint8_t*>(ptrs[i]);
             uint64_t j = i + 1;
-            while (j < n && lens[j] && lens[j - 1] % kAlign == 0 &&
+            while (j < n && lens[j] && off[j] == off[j - 1] + lens[j - 1] &&
                    static_cast<const uint8_t*>(ptrs[j]) == static_cast<const uint8_t*>(ptrs[j - 1]) + lens[j - 1])
                 j++;
             const uint64_t bytes = off[j - 1] - off[i] + lens[j - 1];
@@ -469,6 +461,22 @@ int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens
     RC_TRY(flush());
     HIP_TRY(hipStreamSynchronize(d.copy));
     return DM_OK;
+}
+
+// Pack host chunks into device memory (256-B aligned starts) through the pinned ring.
+// Returns the device address of each chunk in `addr`.
+int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uint64_t n,
+                std::vector<uint64_t>& addr) {
+    std::vector<uint64_t> off(n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        off[i] = total;
+        total = round_up(total + lens[i], kAlign);
+    }
+    HIP_TRY(d.data.ensure(std::max<uint64_t>(total, kAlign)));
+    addr.resize(n);
+    for (uint64_t i = 0; i < n; i++) addr[i] = reinterpret_cast<uint64_t>(d.data.u8() + off[i]);
+    return h2d_at(c, d, ptrs, lens, n, off);
 }
 
 // Host object buffer -> HBM, hashing overlapped with the H2D copies.  Leaf digests land in
@@ -1021,3 +1029,4 @@ int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t*
 #include "rs_capi.inl"
 #include "process_capi.inl"
 #include "tree_capi.inl"
+#include "batcher.inl"

@@ -16,13 +16,15 @@
 
 namespace {
 
-int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uint64_t segment, uint8_t* parity,
-                uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t* fid) {
+// nseg segments at `obj` (segment-contiguous, padding already zeroed) belonging to objects whose
+// segments start at first[o] (first.size() == nobj + 1): RS coding, one leaf launch over every
+// segment and fragment, one fid per object into fids (nobj x 32, device).  Digests land in
+// d.leaves: segment s at s, fragment (s, j) at nseg + s * total + j.
+int process_segments(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t segment, uint8_t* parity,
+                     const std::vector<uint64_t>& first, uint8_t* fids) {
     dm_ctx* c = r->c;
     const int k = r->k, m = r->m, total = k + m;
-    const uint64_t nseg = ceil_div(len, segment), frag = segment / (uint64_t)k;
-    RC_TRY(begin_call(c, d, s));
-    if (nseg * segment > len) HIP_TRY(hipMemsetAsync(obj + len, 0, nseg * segment - len, s));
+    const uint64_t nseg = first.back(), frag = segment / (uint64_t)k, nobj = first.size() - 1;
     dm::RsArgs a{};
     for (int j = 0; j < k; j++) a.in[j] = obj + (uint64_t)j * frag;
     for (int i = 0; i < m; i++) a.out[i] = parity + (uint64_t)i * frag;
@@ -34,7 +36,7 @@ int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uin
     a.nout = (uint32_t)m;
     launch_rs(d, s, k, a);
     HIP_TRY(hipGetLastError());
-    // leaf table: segments first, then fragments in (segment, shard) order
+    // leaf table: segments first (their chains are the longest: they start first), then fragments
     const uint64_t T = nseg * (1 + (uint64_t)total);
     std::vector<uint64_t> addr(T), lens(T);
     for (uint64_t i = 0; i < nseg; i++) {
@@ -48,7 +50,7 @@ int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uin
                                                        : parity + (i * m + (j - k)) * frag);
             lens[t] = frag;
         }
-    RC_TRY(tables_begin(c, d, T * 16 + 1024));
+    RC_TRY(tables_begin(c, d, T * 16 + (nobj + 1) * 12 + 2048));
     HIP_TRY(d.leaves.ensure(T * 32));
     RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), T * 8));
     RC_TRY(upload(c, d, s, d.tab_len, lens.data(), T * 8));
@@ -62,11 +64,71 @@ int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uin
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
     RC_TRY(launch_leaves(c, s, la, true, true, pick_leaf_kernel(c, d, T)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
-    RC_TRY(finish(c, d, s, d.leaves.u8(), nseg, true, fid));
+    if (nobj == 1) RC_TRY(finish(c, d, s, d.leaves.u8(), nseg, true, fids));
+    else RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, fids));
     if (tr) HIP_TRY(hipEventRecord(tr[2], s));
+    return DM_OK;
+}
+
+int process_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t len, uint64_t segment, uint8_t* parity,
+                uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t* fid) {
+    dm_ctx* c = r->c;
+    const int total = r->k + r->m;
+    const uint64_t nseg = ceil_div(len, segment);
+    RC_TRY(begin_call(c, d, s));
+    if (nseg * segment > len) HIP_TRY(hipMemsetAsync(obj + len, 0, nseg * segment - len, s));
+    RC_TRY(process_segments(r, d, s, obj, segment, parity, {0, nseg}, fid));
     if (seg_hashes) HIP_TRY(hipMemcpyAsync(seg_hashes, d.leaves.p, nseg * 32, hipMemcpyDeviceToDevice, s));
     if (frag_hashes)
         HIP_TRY(hipMemcpyAsync(frag_hashes, d.leaves.u8() + nseg * 32, nseg * total * 32, hipMemcpyDeviceToDevice, s));
+    return DM_OK;
+}
+
+// Host objects -> device (segment-aligned, zero-padded) -> process_segments -> host outputs.
+// Per-object outputs are nullable (frags_out / seg_hashes / frag_hashes may be NULL arrays or hold
+// NULL entries); fids (nobj x 32) is required.  Runs on d.stream, synchronous.
+int process_host(dm_rs* r, Dev& d, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t segment,
+                 void* const* frags_out, uint8_t* const* seg_hashes, uint8_t* const* frag_hashes, uint8_t* fids) {
+    dm_ctx* c = r->c;
+    hipStream_t s = d.stream;
+    RC_TRY(begin_call(c, d, s));
+    const int k = r->k, m = r->m, total = k + m;
+    const uint64_t frag = segment / (uint64_t)k;
+    std::vector<uint64_t> first(nobj + 1, 0), off(nobj);
+    for (uint64_t o = 0; o < nobj; o++) {
+        first[o + 1] = first[o] + ceil_div(lens[o], segment);
+        off[o] = first[o] * segment;
+    }
+    const uint64_t S = first[nobj];
+    HIP_TRY(d.data.ensure(S * segment + kAlign));
+    RC_TRY(h2d_at(c, d, objs, lens, nobj, off));
+    for (uint64_t o = 0; o < nobj; o++) {
+        const uint64_t pad = (first[o + 1] - first[o]) * segment - lens[o];
+        if (pad) HIP_TRY(hipMemsetAsync(d.data.u8() + off[o] + lens[o], 0, pad, s));
+    }
+    HIP_TRY(r->work.ensure(S * (uint64_t)m * frag + nobj * 32));
+    uint8_t* parity = r->work.u8();
+    uint8_t* dfid = parity + S * (uint64_t)m * frag;
+    RC_TRY(process_segments(r, d, s, d.data.u8(), segment, parity, first, dfid));
+    HIP_TRY(hipMemcpyAsync(fids, dfid, nobj * 32, hipMemcpyDeviceToHost, s));
+    for (uint64_t o = 0; o < nobj; o++) {
+        const uint64_t f0 = first[o], ns = first[o + 1] - first[o];
+        if (seg_hashes && seg_hashes[o])
+            HIP_TRY(hipMemcpyAsync(seg_hashes[o], d.leaves.u8() + f0 * 32, ns * 32, hipMemcpyDeviceToHost, s));
+        if (frag_hashes && frag_hashes[o])
+            HIP_TRY(hipMemcpyAsync(frag_hashes[o], d.leaves.u8() + (S + f0 * total) * 32, ns * total * 32,
+                                   hipMemcpyDeviceToHost, s));
+        if (frags_out && frags_out[o]) {
+            uint8_t* out = static_cast<uint8_t*>(frags_out[o]);
+            for (uint64_t i = 0; i < ns; i++) {
+                HIP_TRY(hipMemcpyAsync(out + i * total * frag, d.data.u8() + (f0 + i) * segment, segment,
+                                       hipMemcpyDeviceToHost, s));
+                HIP_TRY(hipMemcpyAsync(out + i * total * frag + segment, parity + (f0 + i) * m * frag, m * frag,
+                                       hipMemcpyDeviceToHost, s));
+            }
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));
     return DM_OK;
 }
 
@@ -104,33 +166,22 @@ int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment
     std::lock_guard<std::mutex> lk(c->mu);
     if (!fid || (!host && len)) return fail(c, DM_ERR_INVALID, "dm_process_buffer: null argument");
     RC_TRY(process_check(r, len, segment));
-    Dev& d = c->devs[0];
-    hipStream_t s = d.stream;
-    RC_TRY(begin_call(c, d, s));
-    const int k = r->k, m = r->m, total = k + m;
-    const uint64_t nseg = ceil_div(len, segment), frag = segment / (uint64_t)k;
-    HIP_TRY(d.data.ensure(nseg * segment));
-    std::vector<uint64_t> addr;
-    const void* src = host;
-    RC_TRY(pack_chunks(c, d, &src, &len, 1, addr));   // H2D into d.data (offset 0)
-    HIP_TRY(r->work.ensure(nseg * (uint64_t)m * frag + (nseg * (1 + (uint64_t)total) + 1) * 32));
-    uint8_t* parity = r->work.u8();
-    uint8_t* dig = parity + nseg * (uint64_t)m * frag;   // seg hashes, frag hashes, fid
-    RC_TRY(process_dev(r, d, s, d.data.u8(), len, segment, parity, dig, dig + nseg * 32,
-                       dig + nseg * (1 + (uint64_t)total) * 32));
-    HIP_TRY(hipMemcpyAsync(fid, dig + nseg * (1 + (uint64_t)total) * 32, 32, hipMemcpyDeviceToHost, s));
-    if (seg_hashes) HIP_TRY(hipMemcpyAsync(seg_hashes, dig, nseg * 32, hipMemcpyDeviceToHost, s));
-    if (frag_hashes) HIP_TRY(hipMemcpyAsync(frag_hashes, dig + nseg * 32, nseg * total * 32, hipMemcpyDeviceToHost, s));
-    if (frags_out) {
-        uint8_t* o = static_cast<uint8_t*>(frags_out);
-        for (uint64_t i = 0; i < nseg; i++) {
-            HIP_TRY(hipMemcpyAsync(o + i * total * frag, d.data.u8() + i * segment, segment, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(o + i * total * frag + segment, parity + i * m * frag, m * frag,
-                                   hipMemcpyDeviceToHost, s));
-        }
+    return process_host(r, c->devs[0], &host, &len, 1, segment, &frags_out, &seg_hashes, &frag_hashes, fid);
+}
+
+int dm_process_batch(dm_rs* r, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t segment,
+                     void* const* frags_out, uint8_t* const* seg_hashes, uint8_t* const* frag_hashes, uint8_t* fids) {
+    if (!r) return DM_ERR_INVALID;
+    dm_ctx* c = r->c;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (nobj == 0) return DM_OK;
+    if (!objs || !lens || !fids) return fail(c, DM_ERR_INVALID, "dm_process_batch: null argument");
+    for (uint64_t o = 0; o < nobj; o++) {
+        if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
+        if (!objs[o]) return fail(c, DM_ERR_INVALID, "object %llu: NULL pointer", (unsigned long long)o);
     }
-    HIP_TRY(hipStreamSynchronize(s));
-    return DM_OK;
+    RC_TRY(process_check(r, lens[0], segment));
+    return process_host(r, c->devs[0], objs, lens, nobj, segment, frags_out, seg_hashes, frag_hashes, fids);
 }
 
 }  // extern "C"

@@ -78,6 +78,45 @@ class Processor:
                     "dm_process_buffer")
         return seg.raw[:32 * nseg], frag.raw[:32 * nseg * total], fid.raw, (frags.raw if frags is not None else None)
 
+    def process_batch(self, bufs, want_frags: bool = False):
+        """``dm_process_batch``: many objects in one pass; list of (seg digests, frag digests, fid,
+        fragments or None) per object."""
+        n = len(bufs)
+        if n == 0:
+            return []
+        total = self.k + self.m
+        srcs, segs, frs, fragss = [], [], [], []
+        ptrs = (ctypes.c_void_p * n)()
+        lens = (ctypes.c_uint64 * n)()
+        sp = (ctypes.c_void_p * n)()
+        fp = (ctypes.c_void_p * n)()
+        gp = (ctypes.c_void_p * n)()
+        for i, b in enumerate(bufs):
+            nseg = (len(b) + self.segment - 1) // self.segment
+            src = ctypes.create_string_buffer(bytes(b), max(len(b), 1))
+            srcs.append(src)
+            ptrs[i] = ctypes.addressof(src)
+            lens[i] = len(b)
+            segs.append(ctypes.create_string_buffer(max(32 * nseg, 32)))
+            frs.append(ctypes.create_string_buffer(max(32 * nseg * total, 32)))
+            sp[i] = ctypes.addressof(segs[-1])
+            fp[i] = ctypes.addressof(frs[-1])
+            if want_frags and nseg:
+                fragss.append(ctypes.create_string_buffer(nseg * total * self.frag))
+                gp[i] = ctypes.addressof(fragss[-1])
+            else:
+                fragss.append(None)
+                gp[i] = None
+        fids = ctypes.create_string_buffer(32 * n)
+        self._check(self.ctx._L.dm_process_batch(self.enc._h, ptrs, lens, n, self.segment, gp, sp, fp, fids),
+                    "dm_process_batch")
+        out = []
+        for i, b in enumerate(bufs):
+            nseg = (len(b) + self.segment - 1) // self.segment
+            out.append((segs[i].raw[:32 * nseg], frs[i].raw[:32 * nseg * total], fids.raw[32 * i:32 * i + 32],
+                        fragss[i].raw if fragss[i] is not None else None))
+        return out
+
     def process_device_async(self, obj_ptr: int, length: int, parity_ptr: int, seg_hash_ptr: int,
                              frag_hash_ptr: int, fid_ptr: int, stream: int = 0) -> None:
         """``dm_process_device_async``: object already in HBM (room for whole segments)."""

@@ -181,6 +181,12 @@ int dm_process_device_async(dm_rs *rs, void *dev_obj, uint64_t len, uint64_t seg
  * frag_hashes nseg x (data + parity) x 32 are nullable; fid is required. */
 int dm_process_buffer(dm_rs *rs, const void *host, uint64_t len, uint64_t segment, void *frags_out,
                       uint8_t *seg_hashes, uint8_t *frag_hashes, uint8_t fid[32]);
+/* Many objects in one pass (the batch upload PUT /files, node/filesHandler.go:197-288, runs
+ * FullProcessing per file): every segment of every object in one RS launch and one leaf launch.
+ * Per-object outputs as in dm_process_buffer (frags_out, seg_hashes, frag_hashes: arrays of nobj
+ * pointers, the arrays or their entries nullable); fids: nobj x 32 bytes. */
+int dm_process_batch(dm_rs *rs, const void *const *objs, const uint64_t *lens, uint64_t nobj, uint64_t segment,
+                     void *const *frags_out, uint8_t *const *seg_hashes, uint8_t *const *frag_hashes, uint8_t *fids);
 
 /* ---- Merkle tree levels and proofs ----------------------------------------
  * cbergoon/merkletree v0.2.0 (go.mod:10) keeps every node of the tree NewHashTree returns
@@ -215,6 +221,31 @@ int dm_verify_object_device_async(dm_ctx *ctx, const void *dev_obj, uint64_t len
                                   uint64_t root_stride, void *dev_ok, void *stream);
 int dm_verify_paths(dm_ctx *ctx, const void *const *contents, const uint64_t *lens, uint64_t q, const uint8_t *paths,
                     const uint8_t *bits, uint32_t depth, const uint8_t *roots, uint64_t root_stride, uint8_t *ok);
+
+/* ---- coalescing executor for concurrent callers ------------------------------------------------
+ * Upload handlers run one goroutine per request, each hashing / processing its own object.  A
+ * dm_batcher takes blocking calls from any number of threads and turns whatever is queued into
+ * one batched GPU pass (one leaf launch over every request's leaves, one tree per request), on
+ * `slots` worker contexts so one batch collects while another runs.  Results are identical to
+ * the single-object calls (dm_root_buffer / dm_process_buffer). */
+typedef struct dm_batcher dm_batcher;
+enum { DM_BATCH_ROOT = 0, DM_BATCH_PROCESS = 1 };
+/* mode ROOT: unit = chunk size (each request: NewHashTreeFromBuffer); PROCESS: unit = segment size
+ * with data/parity shards (each request: FullProcessing).  slots (0 = 2) worker contexts on GPU
+ * `device`; max_leaves / max_bytes per batch (0 = 2048 leaves / 16 GiB); linger_us: how long a
+ * worker waits for more requests after the first before launching (0 = at once). */
+int dm_batcher_create(int device, int mode, uint64_t unit, int data_shards, int parity_shards, int slots,
+                      uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher **out);
+/* Drains queued requests, then frees the workers and their contexts. */
+void dm_batcher_destroy(dm_batcher *b);
+/* Blocking, thread-safe.  Same outputs as dm_root_buffer (leaf_out nullable) / dm_process_buffer. */
+int dm_batcher_root(dm_batcher *b, const void *host, uint64_t len, uint8_t *leaf_out, uint8_t root[32]);
+int dm_batcher_process(dm_batcher *b, const void *host, uint64_t len, void *frags_out, uint8_t *seg_hashes,
+                       uint8_t *frag_hashes, uint8_t fid[32]);
+/* Requests served, batches launched, largest batch (requests). */
+int dm_batcher_stats(dm_batcher *b, uint64_t *requests, uint64_t *batches, uint64_t *max_batch);
+/* Message of the calling thread's last failing dm_batcher_* call. */
+const char *dm_batcher_last_error(void);
 
 /* ---- tuning ------------------------------------------------------------------------------ */
 

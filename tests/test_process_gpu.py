@@ -276,3 +276,90 @@ def test_hashtree_mirror_proof_api(ctx, tmp_path):
     assert tree.VerifyTree() == (True, None)
     tree.Leafs[2].C.x = b"tampered"
     assert tree.VerifyTree() == (False, None)
+
+
+# ---- batched FullProcessing and the coalescing executor -------------------------------------------
+
+def test_process_batch_matches_oracle(ctx, oracle_lib):
+    from oracle import splitmix64_bytes
+    p = _processor(ctx, 4, 8, 4096)
+    rng = random.Random(11)
+    bufs = [splitmix64_bytes(rng.choice([1, 63, 4096, 4097, 9000, 3 * 4096, 50000]), 0xDE0552400 + i)
+            for i in range(23)]
+    got = p.process_batch(bufs, want_frags=True)
+    for b, (seg, frag, fid, frags) in zip(bufs, got):
+        ws, wf, wfid, wfr = oracle_lib.full_processing(b, 4096, 4, 8, want_frags=True)
+        assert (seg, frag, fid, frags) == (ws, wf, wfid, wfr)
+    from deoss_amd import DeossMerkleError
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        p.process_batch([b"abc", b""])
+    p.close()
+
+
+def test_batcher_root_concurrent(oracle_lib):
+    """64 threads x 4 blocking requests of random size: every root equals the oracle's, and the
+    requests were coalesced into fewer launches."""
+    import threading
+    from deoss_amd.batcher import ROOT, Batcher
+    from oracle import splitmix64_bytes
+    chunk = 64 << 10
+    b = Batcher(ROOT, chunk, slots=2, linger_us=200)
+    errors, results = [], {}
+
+    def worker(t):
+        rng = random.Random(t)
+        try:
+            for r in range(4):
+                n = rng.choice([1, 100, chunk - 1, chunk, chunk + 1, 3 << 20, (1 << 20) + 7])
+                data = splitmix64_bytes(n, 0xDE0552500 + 16 * t + r)
+                leaves, root = b.root(data, want_leaves=True)
+                results[(t, r)] = (data, leaves, root)
+        except Exception as e:   # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    assert len(results) == 256
+    for data, leaves, root in results.values():
+        wl, wr = oracle_lib.root_buffer(data, chunk)
+        assert (leaves, root) == (wl, wr)
+    nreq, nbatch, maxb = b.stats()
+    assert nreq == 256 and nbatch < nreq and maxb > 1
+    b.close()
+
+
+def test_batcher_process_concurrent(oracle_lib):
+    import threading
+    from deoss_amd.batcher import PROCESS, Batcher
+    from oracle import splitmix64_bytes
+    b = Batcher(PROCESS, 4096, 4, 8, slots=3, linger_us=100)
+    errors, results = [], []
+
+    def worker(t):
+        try:
+            for r in range(3):
+                data = splitmix64_bytes(1 + (t * 7919 + r * 104729) % 20000, 0xDE0552600 + 8 * t + r)
+                results.append((data, b.process(data, want_frags=True)))
+        except Exception as e:
+            errors.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(24)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for data, got in results:
+        assert got == oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
+    nreq, nbatch, _ = b.stats()
+    assert nreq == 72 and nbatch < nreq
+    from deoss_amd import DeossMerkleError
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        b.process(b"")
+    with pytest.raises(DeossMerkleError):
+        b.root(b"x")          # wrong mode
+    b.close()
