@@ -5,8 +5,10 @@
 // (node/objectHandler.go:168, node/fileHandler.go:771, node/filesHandler.go:201,
 // node/resumeHandler.go:326, node/tracker.go:767-769) and the fragment download path re-runs
 // (node/fileHandler.go:964,997).  Same signature and result shape; segmenting, Reed-Solomon 4 + 8
-// coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h,
-// dm_process_buffer and dm_tree_levels).  Swap it in by changing the handlers' import of
+// coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h): calls
+// from concurrent handler goroutines go through one dm_batcher, which coalesces whatever is
+// queued into one batched GPU pass (dm_batcher_process), and dm_tree_levels builds the fid of
+// files larger than one window.  Swap it in by changing the handlers' import of
 // github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
 // Deviations: cipher must be "" (the AES branch is not implemented), and segment files are not
 // written (their bytes are the data fragments in order).  Build with `-tags hip`, CGO_ENABLED=1.
@@ -26,6 +28,7 @@ import (
 	"io"
 	"os"
 	"path/filepath"
+	"runtime"
 	"sync"
 	"unsafe"
 
@@ -36,11 +39,10 @@ import (
 const windowSegments = 64
 
 var (
-	once   sync.Once
-	ctx    *C.dm_ctx
-	rs     *C.dm_rs
-	initEr error
-	mu     sync.Mutex // dm_rs calls serialise on the context anyway; keeps buffers per call simple
+	once    sync.Once
+	ctx     *C.dm_ctx     // tree levels over the segment digests of multi-window files
+	batcher *C.dm_batcher // FullProcessing requests from every goroutine
+	initEr  error
 )
 
 func gpu() error {
@@ -49,17 +51,28 @@ func gpu() error {
 			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
 			return
 		}
-		if rc := C.dm_rs_create(ctx, C.int(chain.DataShards), C.int(chain.ParShards), &rs); rc != C.DM_OK {
-			initEr = errors.New(C.GoString(C.dm_last_error(ctx)))
+		// 2 worker slots, 2048 leaves per batch, 2 ms linger (DESIGN.md "coalescing executor")
+		if rc := C.dm_batcher_create(0, C.DM_BATCH_PROCESS, C.uint64_t(chain.SegmentSize), C.int(chain.DataShards),
+			C.int(chain.ParShards), 0, 0, 0, 2000, &batcher); rc != C.DM_OK {
+			initEr = errors.New(C.GoString(C.dm_batcher_last_error()))
 		}
 	})
 	return initEr
 }
 
-func rcError(rc C.int) error {
+// batcherError must run on the goroutine's OS thread that made the call (the message is
+// thread-local in the library): callers hold runtime.LockOSThread around the pair.
+func batcherError(rc C.int) error {
 	if rc == C.DM_ERR_EMPTY {
 		return errors.New("Empty data")
 	}
+	if msg := C.GoString(C.dm_batcher_last_error()); msg != "" {
+		return errors.New(msg)
+	}
+	return errors.New(C.GoString(C.dm_strerror(rc)))
+}
+
+func ctxError(rc C.int) error {
 	if msg := C.GoString(C.dm_last_error(ctx)); msg != "" {
 		return errors.New(msg)
 	}
@@ -81,18 +94,27 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		return nil, "", err
 	}
 	defer f.Close()
+	st, err := f.Stat()
+	if err != nil {
+		return nil, "", err
+	}
+	if st.Size() == 0 {
+		return nil, "", errors.New("Empty data")
+	}
 	if err = os.MkdirAll(savedir, 0755); err != nil {
 		return nil, "", err
 	}
 	seg := uint64(chain.SegmentSize)
 	total := chain.DataShards + chain.ParShards
 	frag := seg / uint64(chain.DataShards)
-	window := make([]byte, windowSegments*seg)
+	wsize := windowSegments * seg // a small upload reads into a buffer of its own size
+	if uint64(st.Size()) < wsize {
+		wsize = uint64(st.Size())
+	}
+	window := make([]byte, wsize)
 	var info []chain.SegmentDataInfo
 	var segDigests []byte
 	var fid [32]byte
-	mu.Lock()
-	defer mu.Unlock()
 	for {
 		n, rerr := io.ReadFull(f, window)
 		if n == 0 {
@@ -105,11 +127,17 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		frags := make([]byte, nseg*uint64(total)*frag)
 		segd := make([]byte, 32*nseg)
 		fragd := make([]byte, 32*nseg*uint64(total))
-		rc := C.dm_process_buffer(rs, unsafe.Pointer(&window[0]), C.uint64_t(n), C.uint64_t(seg),
-			unsafe.Pointer(&frags[0]), (*C.uint8_t)(unsafe.Pointer(&segd[0])),
-			(*C.uint8_t)(unsafe.Pointer(&fragd[0])), (*C.uint8_t)(unsafe.Pointer(&fid[0])))
+		runtime.LockOSThread()
+		rc := C.dm_batcher_process(batcher, unsafe.Pointer(&window[0]), C.uint64_t(n), unsafe.Pointer(&frags[0]),
+			(*C.uint8_t)(unsafe.Pointer(&segd[0])), (*C.uint8_t)(unsafe.Pointer(&fragd[0])),
+			(*C.uint8_t)(unsafe.Pointer(&fid[0])))
+		var perr error
 		if rc != C.DM_OK {
-			return nil, "", rcError(rc)
+			perr = batcherError(rc)
+		}
+		runtime.UnlockOSThread()
+		if perr != nil {
+			return nil, "", perr
 		}
 		for s := uint64(0); s < nseg; s++ {
 			names := make([]string, total)
@@ -137,7 +165,7 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		nodes := make([]byte, 32*uint64(C.dm_tree_node_count(C.uint64_t(len(info)))))
 		if rc := C.dm_tree_levels(ctx, (*C.uint8_t)(unsafe.Pointer(&segDigests[0])), C.uint64_t(len(info)),
 			(*C.uint8_t)(unsafe.Pointer(&nodes[0]))); rc != C.DM_OK {
-			return nil, "", rcError(rc)
+			return nil, "", ctxError(rc)
 		}
 		copy(fid[:], nodes[len(nodes)-32:])
 	}

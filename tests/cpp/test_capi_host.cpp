@@ -5,6 +5,7 @@
 // Prints PASS and exits 0 when everything matches.
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -295,6 +296,71 @@ int main() {
         EXPECT(dm_process_buffer(rs, nullptr, 0, seg, nullptr, nullptr, nullptr, fid) == DM_ERR_EMPTY);
         EXPECT(dm_process_buffer(rs, fid, 1, 100, nullptr, nullptr, nullptr, fid) == DM_ERR_INVALID);
         dm_rs_destroy(rs);
+    }
+
+    // batched FullProcessing and the coalescing executor (12 threads x 3 blocking requests)
+    {
+        dm_rs* rs = nullptr;
+        EXPECT(dm_rs_create(c, 4, 8, &rs) == DM_OK);
+        const uint64_t seg = 4096, frag = 1024;
+        std::vector<std::vector<uint8_t>> objs;
+        for (int i = 0; i < 9; i++) objs.push_back(bytes(1 + (uint64_t)i * 3001, 8800 + i));
+        std::vector<const void*> op;
+        std::vector<uint64_t> ol;
+        std::vector<std::vector<uint8_t>> gs(9), gf(9);
+        std::vector<uint8_t*> sp(9), fp(9);
+        for (int i = 0; i < 9; i++) {
+            op.push_back(objs[i].data());
+            ol.push_back(objs[i].size());
+            const uint64_t ns = (ol[i] + seg - 1) / seg;
+            gs[i].resize(32 * ns);
+            gf[i].resize(32 * ns * 12);
+            sp[i] = gs[i].data();
+            fp[i] = gf[i].data();
+        }
+        std::vector<uint8_t> fids(32 * 9);
+        EXPECT(dm_process_batch(rs, op.data(), ol.data(), 9, seg, nullptr, sp.data(), fp.data(), fids.data()) == DM_OK);
+        for (int i = 0; i < 9; i++) {
+            const uint64_t ns = (ol[i] + seg - 1) / seg;
+            std::vector<uint8_t> ws(32 * ns), wf(32 * ns * 12);
+            uint8_t wfid[32];
+            or_full_processing(op[i], ol[i], seg, 4, 8, ws.data(), wf.data(), wfid, nullptr, 1);
+            EXPECT(ws == gs[i] && wf == gf[i] && std::memcmp(wfid, fids.data() + 32 * i, 32) == 0);
+        }
+        dm_rs_destroy(rs);
+
+        dm_batcher* bp = nullptr;
+        EXPECT(dm_batcher_create(0, DM_BATCH_PROCESS, seg, 4, 8, 2, 0, 0, 100, &bp) == DM_OK);
+        dm_batcher* br = nullptr;
+        EXPECT(dm_batcher_create(0, DM_BATCH_ROOT, 4096, 0, 0, 3, 64, 0, 0, &br) == DM_OK);
+        std::vector<std::thread> ts;
+        std::atomic<int> bad{0};
+        for (int t = 0; t < 12; t++)
+            ts.emplace_back([&, t] {
+                for (int r = 0; r < 3; r++) {
+                    auto o = bytes(1 + (uint64_t)(t * 7 + r) * 1777, 9900 + t * 3 + r);
+                    uint8_t fid[32], wfid[32], root[32], wroot[32];
+                    const uint64_t ns = (o.size() + seg - 1) / seg;
+                    std::vector<uint8_t> fr(ns * 12 * frag), wfr(ns * 12 * frag), ws(32 * ns), wf(32 * ns * 12);
+                    if (dm_batcher_process(bp, o.data(), o.size(), fr.data(), nullptr, nullptr, fid) != DM_OK) bad++;
+                    or_full_processing(o.data(), o.size(), seg, 4, 8, ws.data(), wf.data(), wfid, wfr.data(), 1);
+                    if (std::memcmp(fid, wfid, 32) != 0 || fr != wfr) bad++;
+                    std::vector<uint8_t> lv(32 * ((o.size() + 4095) / 4096)), wl(lv.size());
+                    if (dm_batcher_root(br, o.data(), o.size(), lv.data(), root) != DM_OK) bad++;
+                    or_root_buffer(o.data(), o.size(), 4096, wl.data(), wroot, 1);
+                    if (std::memcmp(root, wroot, 32) != 0 || lv != wl) bad++;
+                }
+            });
+        for (auto& x : ts) x.join();
+        EXPECT(bad.load() == 0);
+        uint64_t nreq = 0, nb = 0, mx = 0;
+        EXPECT(dm_batcher_stats(bp, &nreq, &nb, &mx) == DM_OK && nreq == 36 && nb >= 1 && nb <= 36);
+        uint8_t tmp[32];
+        EXPECT(dm_batcher_process(bp, nullptr, 0, nullptr, nullptr, nullptr, tmp) == DM_ERR_EMPTY);
+        EXPECT(std::string(dm_batcher_last_error()) == "Empty data");
+        EXPECT(dm_batcher_root(bp, tmp, 1, nullptr, tmp) == DM_ERR_INVALID);   // wrong mode
+        dm_batcher_destroy(bp);
+        dm_batcher_destroy(br);
     }
 
     // Merkle proofs: levels, paths, verification (host forms)
