@@ -104,7 +104,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_verify_paths_device_async": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
         "dm_verify_paths": ([vp, pvp, pu64, u64, vp, vp, u32, vp, u64, vp], i32),
         "dm_verify_object_device_async": ([vp, vp, u64, u64, vp, vp, u32, vp, u64, vp, vp], i32),
-        "dm_batcher_create": ([i32, i32, u64, i32, i32, i32, u64, u64, u32, ctypes.POINTER(vp)], i32),
+        "dm_batcher_create": ([ctypes.POINTER(i32), i32, i32, u64, i32, i32, i32, u64, u64, u32, ctypes.POINTER(vp)],
+                              i32),
         "dm_batcher_destroy": ([vp], None),
         "dm_batcher_root": ([vp, vp, u64, vp, vp], i32),
         "dm_batcher_process": ([vp, vp, u64, vp, vp, vp, vp], i32),

@@ -19,12 +19,15 @@ PROCESS = 1
 
 
 class Batcher:
-    def __init__(self, mode: int, unit: int, data_shards: int = 4, parity_shards: int = 8, device: int = 0,
+    def __init__(self, mode: int, unit: int, data_shards: int = 4, parity_shards: int = 8, device=0,
                  slots: int = 0, max_leaves: int = 0, max_bytes: int = 0, linger_us: int = 0):
+        """device: a GPU ordinal, a list of them (slots per GPU), or None for every visible GPU."""
         self._L = load_library()
         h = ctypes.c_void_p()
-        rc = self._L.dm_batcher_create(device, mode, unit, data_shards, parity_shards, slots, max_leaves, max_bytes,
-                                       linger_us, ctypes.byref(h))
+        devs = None if device is None else ([device] if isinstance(device, int) else list(device))
+        arr = (ctypes.c_int * len(devs))(*devs) if devs else None
+        rc = self._L.dm_batcher_create(arr, len(devs) if devs else 0, mode, unit, data_shards, parity_shards, slots,
+                                       max_leaves, max_bytes, linger_us, ctypes.byref(h))
         if rc != 0:
             raise DeossMerkleError(rc, f"dm_batcher_create: {self._L.dm_batcher_last_error().decode()}")
         self._h = h

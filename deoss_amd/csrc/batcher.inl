@@ -179,11 +179,23 @@ void dm_batcher_destroy(dm_batcher* b) {
     delete b;
 }
 
-int dm_batcher_create(int device, int mode, uint64_t unit, int data_shards, int parity_shards, int slots,
-                      uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher** out) {
+int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int data_shards, int parity_shards,
+                      int slots, uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher** out) {
     if (!out) return DM_ERR_INVALID;
     *out = nullptr;
-    if ((mode != DM_BATCH_ROOT && mode != DM_BATCH_PROCESS) || unit == 0 || slots < 0 || slots > 8) {
+    std::vector<int> dl;
+    if (devs) {
+        dl.assign(devs, devs + std::max(ndev, 0));
+    } else {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+            (void)hipGetLastError();
+            t_batcher_err = "dm_batcher_create: no usable GPU";
+            return DM_ERR_NODEV;
+        }
+        for (int i = 0; i < n; i++) dl.push_back(i);
+    }
+    if (dl.empty() || (mode != DM_BATCH_ROOT && mode != DM_BATCH_PROCESS) || unit == 0 || slots < 0 || slots > 8) {
         t_batcher_err = "dm_batcher_create: bad mode, unit or slot count";
         return DM_ERR_INVALID;
     }
@@ -202,10 +214,11 @@ int dm_batcher_create(int device, int mode, uint64_t unit, int data_shards, int 
     b->max_leaves = max_leaves ? max_leaves : 2048;
     b->max_bytes = max_bytes ? max_bytes : (16ull << 30);
     b->linger_us = linger_us;
-    const int ns = slots ? slots : 2;
-    for (int i = 0; i < ns; i++) {
+    const int per = slots ? slots : 2;
+    const int ns = per * (int)dl.size();
+    for (int i = 0; i < ns; i++) {   // slot i on device dl[i % ndev]: consecutive slots alternate GPUs
         dm_ctx* c = nullptr;
-        int rc = dm_create(&c, &device, 1);
+        int rc = dm_create(&c, &dl[i % dl.size()], 1);
         if (rc != DM_OK) {
             t_batcher_err = std::string("dm_batcher_create: ") + dm_strerror(rc);
             dm_batcher_destroy(b);

@@ -230,12 +230,14 @@ int dm_verify_paths(dm_ctx *ctx, const void *const *contents, const uint64_t *le
  * the single-object calls (dm_root_buffer / dm_process_buffer). */
 typedef struct dm_batcher dm_batcher;
 enum { DM_BATCH_ROOT = 0, DM_BATCH_PROCESS = 1 };
-/* mode ROOT: unit = chunk size (each request: NewHashTreeFromBuffer); PROCESS: unit = segment size
- * with data/parity shards (each request: FullProcessing).  slots (0 = 2) worker contexts on GPU
- * `device`; max_leaves / max_bytes per batch (0 = 2048 leaves / 16 GiB); linger_us: how long a
- * worker waits for more requests after the first before launching (0 = at once). */
-int dm_batcher_create(int device, int mode, uint64_t unit, int data_shards, int parity_shards, int slots,
-                      uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher **out);
+/* devs / ndev: GPUs to serve from (devs NULL: every visible GPU); objects are independent, so
+ * requests spread over the GPUs with no exchange.  mode ROOT: unit = chunk size (each request:
+ * NewHashTreeFromBuffer); PROCESS: unit = segment size with data/parity shards (each request:
+ * FullProcessing).  slots (0 = 2) worker contexts per GPU; max_leaves / max_bytes per batch
+ * (0 = 2048 leaves / 16 GiB); linger_us: how long a worker waits for more requests after the
+ * first before launching (0 = at once). */
+int dm_batcher_create(const int *devs, int ndev, int mode, uint64_t unit, int data_shards, int parity_shards,
+                      int slots, uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher **out);
 /* Drains queued requests, then frees the workers and their contexts. */
 void dm_batcher_destroy(dm_batcher *b);
 /* Blocking, thread-safe.  Same outputs as dm_root_buffer (leaf_out nullable) / dm_process_buffer. */

@@ -330,9 +330,10 @@ int main() {
         dm_rs_destroy(rs);
 
         dm_batcher* bp = nullptr;
-        EXPECT(dm_batcher_create(0, DM_BATCH_PROCESS, seg, 4, 8, 2, 0, 0, 100, &bp) == DM_OK);
+        const int dev0[2] = {0, 0};   // the same GPU twice: slots of two "devices"
+        EXPECT(dm_batcher_create(dev0, 2, DM_BATCH_PROCESS, seg, 4, 8, 1, 0, 0, 100, &bp) == DM_OK);
         dm_batcher* br = nullptr;
-        EXPECT(dm_batcher_create(0, DM_BATCH_ROOT, 4096, 0, 0, 3, 64, 0, 0, &br) == DM_OK);
+        EXPECT(dm_batcher_create(nullptr, 0, DM_BATCH_ROOT, 4096, 0, 0, 3, 64, 0, 0, &br) == DM_OK);
         std::vector<std::thread> ts;
         std::atomic<int> bad{0};
         for (int t = 0; t < 12; t++)

@@ -303,7 +303,7 @@ def test_batcher_root_concurrent(oracle_lib):
     from deoss_amd.batcher import ROOT, Batcher
     from oracle import splitmix64_bytes
     chunk = 64 << 10
-    b = Batcher(ROOT, chunk, slots=2, linger_us=200)
+    b = Batcher(ROOT, chunk, device=None, slots=2, linger_us=200)   # every visible GPU
     errors, results = [], {}
 
     def worker(t):
@@ -336,7 +336,7 @@ def test_batcher_process_concurrent(oracle_lib):
     import threading
     from deoss_amd.batcher import PROCESS, Batcher
     from oracle import splitmix64_bytes
-    b = Batcher(PROCESS, 4096, 4, 8, slots=3, linger_us=100)
+    b = Batcher(PROCESS, 4096, 4, 8, device=[0, 0], slots=2, linger_us=100)   # 2 'GPUs' x 2 slots
     errors, results = [], []
 
     def worker(t):
