@@ -707,7 +707,7 @@ def run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo):
                                f"{'chunk' if args.mode == 'root' else 'segment'} {unit} B ({args.mode})",
                    "threads": args.threads, "requests": nreq, "object_bytes": obj, "unit": unit},
         "batcher": {"seconds": round(res["batcher"], 4), "requests": stats[0], "batches": stats[1],
-                    "largest_batch": stats[2], "slots": args.slots or 2, "max_leaves": args.max_leaves or 2048,
+                    "largest_batch": stats[2], "slots": args.slots or 2, "max_leaves": args.max_leaves or 4096,
                     "linger_us": args.linger_us},
         "parity": {"checked": check, "mismatches": int(mism), "bit_exact": mism == 0},
     }

@@ -209,9 +209,9 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
     b->unit = unit;
     b->k = data_shards;
     b->m = parity_shards;
-    // default budget: half of what K1Q keeps resident (two 64 KiB workgroups x 8 leaves per CU),
+    // default budget: half of what K1Q keeps resident (four 37 KiB workgroups x 8 leaves per CU),
     // so two slots' batches fit side by side
-    b->max_leaves = max_leaves ? max_leaves : 2048;
+    b->max_leaves = max_leaves ? max_leaves : 4096;
     b->max_bytes = max_bytes ? max_bytes : (16ull << 30);
     b->linger_us = linger_us;
     const int per = slots ? slots : 2;

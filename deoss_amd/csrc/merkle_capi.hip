@@ -234,14 +234,13 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // Leaf-kernel choice for a uniform-chunk object of n leaves: the more lanes a kernel spends per
 // leaf, the shorter each leaf's serial chain, as long as its workgroups fit the chip at once.
 // Returns DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR or DM_LEAF_QUAD.
-// Measured on MI355X (profiles/r01_crossover_quad.log, 8 GiB object): K1Q wins up to 4,096
-// leaves (two 64 KiB-LDS workgroups per CU, each consumer wave on its own SIMD), K1P up to
-// 8,192 (one workgroup per CU), K1L up to 16,384; past that one lane per leaf with >= 2 waves
-// per SIMD wins.
+// Measured on MI355X (8 GiB object, profiles/r01_sweep_k1q4.log): K1Q wins up to 8,192 leaves
+// (four 37 KiB-LDS workgroups per CU: 345.6 GiB/s at 8,192 leaves vs 274.7 for K1P), K1L up to
+// 16,384 (536 vs 397 for K1P, 223 for K1Q in two rounds of workgroups); past that one lane per
+// leaf with >= 2 waves per SIMD wins.  K1P stays selectable (DM_LEAF_PAIR).
 int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
     if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
-    if (ceil_div(n, dm::kQuadLeaves) <= 2 * (uint64_t)d.cus) return DM_LEAF_QUAD;
-    if (ceil_div(n, dm::kPairLeaves) <= (uint64_t)d.cus) return DM_LEAF_PAIR;
+    if (ceil_div(n, dm::kQuadLeaves) <= 4 * (uint64_t)d.cus) return DM_LEAF_QUAD;
     if (ceil_div(n, dm::kLatLeaves) <= (uint64_t)d.cus) return DM_LEAF_LATENCY;
     return DM_LEAF_WIDE;
 }
@@ -263,7 +262,9 @@ void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
                            0, s, la);
 }
 
-// Launch the chosen leaf kernel (K1 / K1L / K1P / K1Q) over la's leaves.
+// Launch the chosen leaf kernel (K1 / K1L / K1P / K1Q) over la's leaves.  (K1Q workgroups fit
+// four to a CU; padding them with dynamic LDS to force two per CU was measured to change nothing
+// at <= 4,096 leaves: the dispatcher already spreads them.)
 int launch_leaves(dm_ctx* c, hipStream_t s, const dm::LeafArgs& la, bool table, bool aligned, int kind) {
     if (table) {
         if (aligned) launch_leaves_t<true, true>(s, la, kind);
@@ -656,7 +657,8 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
     // per-device: H2D of its byte range + subtree to k levels (parallel host threads)
     auto work = [&](int g) {
         Dev& d = c->devs[g];
-        dm_ctx local;   // private error sink
+        dm_ctx local;   // private error sink (no devices: helpers given it must not index devs)
+        local.leaf_mode = c->leaf_mode;
         dm_ctx* cc = &local;
         int rc = DM_OK;
         do {

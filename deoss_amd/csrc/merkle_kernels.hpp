@@ -52,14 +52,31 @@ __device__ __forceinline__ void store_digest(uint8_t* p, const uint32_t (&v)[8])
 // Load one 64-byte block (16 B aligned) as 4 vector loads.
 struct Blk { uint4 q0, q1, q2, q3; };
 
+// Leaf bytes always live in global memory.  Table-mode leaf pointers come from memory, so the
+// compiler cannot infer their address space: without the cast it emits FLAT loads (split into
+// dwordx3/x4/x1 pieces, counted against lgkmcnt with the LDS traffic), which cost K1Q's producer
+// 9 % in table mode (batches of 4,096 leaves: 46.0 vs 42.1 ms).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4_t global_u32x4;
+
+typedef __attribute__((address_space(1))) const uint8_t global_u8;
+typedef __attribute__((address_space(1))) const uint32_t global_u32;
+
+__device__ __forceinline__ uint4 to_uint4(u32x4_t v) { return make_uint4(v.x, v.y, v.z, v.w); }
+__device__ __forceinline__ const global_u8* gbytes(const uint8_t* p) { return (const global_u8*)p; }
+
 template <bool ALIGNED>
 __device__ __forceinline__ Blk load_block(const uint8_t* p) {
     Blk b;
     if constexpr (ALIGNED) {
-        const uint4* q = reinterpret_cast<const uint4*>(p);
-        b.q0 = q[0]; b.q1 = q[1]; b.q2 = q[2]; b.q3 = q[3];
+        const global_u32x4* q = (const global_u32x4*)(p);
+        b.q0 = to_uint4(q[0]); b.q1 = to_uint4(q[1]); b.q2 = to_uint4(q[2]); b.q3 = to_uint4(q[3]);
     } else {
-        __builtin_memcpy(&b, p, 64);
+        uint8_t t[64];
+        const global_u8* g = gbytes(p);
+#pragma unroll
+        for (int k = 0; k < 64; k++) t[k] = g[k];
+        __builtin_memcpy(&b, t, 64);
     }
     return b;
 }
@@ -95,17 +112,18 @@ __device__ __forceinline__ void absorb_tail(uint32_t (&st)[8], const uint8_t* p,
         uint32_t v = 0;
         if ((uint32_t)(4 * k + 4) <= r) {
             if constexpr (ALIGNED) {
-                v = bswap32(*reinterpret_cast<const uint32_t*>(p + 4 * k));
+                v = bswap32(*(const global_u32*)(p + 4 * k));
             } else {
-                v = ((uint32_t)p[4 * k] << 24) | ((uint32_t)p[4 * k + 1] << 16) |
-                    ((uint32_t)p[4 * k + 2] << 8) | (uint32_t)p[4 * k + 3];
+                const global_u8* g = gbytes(p);
+                v = ((uint32_t)g[4 * k] << 24) | ((uint32_t)g[4 * k + 1] << 16) |
+                    ((uint32_t)g[4 * k + 2] << 8) | (uint32_t)g[4 * k + 3];
             }
         } else if ((uint32_t)(4 * k) <= r) {
             // word holding the 0x80 terminator (and 0..3 message bytes)
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 uint32_t idx = 4 * k + j;
-                uint32_t byte = idx < r ? (uint32_t)p[idx] : (idx == r ? 0x80u : 0u);
+                uint32_t byte = idx < r ? (uint32_t)gbytes(p)[idx] : (idx == r ? 0x80u : 0u);
                 v |= byte << (24 - 8 * j);
             }
         }
@@ -526,6 +544,13 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
 constexpr int kQuadLeaves = 8;      // leaves per workgroup (8 consumer lanes per leaf)
 constexpr int kQuadBlocks = 8;      // blocks per leaf per ring stage (one producer lane each)
 constexpr int kQuadFuseMax = 3;     // 8 leaves -> 1 node
+// LDS row of one (round group, block): K+W of the 8 leaves, then one (1,1,1,1) entry that every
+// a-triple lane reads (broadcast) as the "+1" of its -d = ~d + 1.  37 KiB per workgroup: 4
+// workgroups fit a CU's 160 KiB.
+constexpr int kQuadRow = kQuadLeaves + 1;
+constexpr int kQuadG = kQuadBlocks * kQuadRow;   // uint4 per round-group row
+constexpr size_t kQuadLdsBytes = sizeof(uint4) * kLatRing * 16 * kQuadG + 4 * 8 * kQuadLeaves + 4 * 8 * (kQuadLeaves / 2);
+static_assert(4 * kQuadLdsBytes <= (160u << 10), "four K1Q workgroups must fit a CU's LDS");
 
 // One round, hand-scheduled: hipcc re-associates the two DPP xors and cannot fold a bank-masked
 // DPP move into its add, so the round is written out.  H (= X7 ^ N + V, then + d on the e-triple)
@@ -551,10 +576,10 @@ constexpr int kQuadFuseMax = 3;     // 8 leaves -> 1 node
 // last round of a block: the next H depends on the feed-forward, so just wait
 #define DM_QUAD_NO_NEXT "s_nop 1\n\t"
 
-// 64 rounds of one block from the ring (kw: this lane's column, stride kQuadBlocks*kQuadLeaves).
+// 64 rounds of one block from the ring (kw: this lane's entry, stride kQuadG per round group).
 __device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
                                                     uint32_t neg) {
-    constexpr int G = kQuadBlocks * kQuadLeaves;
+    constexpr int G = kQuadG;
     uint32_t x4 = x[0], x5 = x[1], x6 = x[2], x7 = x[3];
     uint32_t r_, f_, s_, h;
     uint4 q = kw[0];
@@ -584,9 +609,9 @@ __device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint
 
 template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
-    constexpr int G = kQuadBlocks * kQuadLeaves;              // uint4 per group row
-    // [role: 0 = K+W, 1 = ones][stage][group][block][leaf]
-    __shared__ uint4 ring[2][kLatRing][16][G];
+    constexpr int G = kQuadG;                                 // uint4 per group row
+    // [stage][group][block][leaf 0..7 = K+W, 8 = ones]
+    __shared__ uint4 ring[kLatRing][16][G];
     __shared__ uint32_t lds_a[kQuadLeaves][8];
     __shared__ uint32_t lds_b[kQuadLeaves / 2][8];
     const uint32_t lane = threadIdx.x & 63;
@@ -598,10 +623,8 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     const LeafView v = leaf_view<TABLE>(a, i);
     const uint64_t NB = wave_max_u64(v.nb);
     const uint64_t NI = (NB + kQuadBlocks - 1) / kQuadBlocks;
-    {
-        uint4* ones = &ring[1][0][0][0];
-        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * G; t += kLatThreads) ones[t] = make_uint4(1, 1, 1, 1);
-    }
+    for (uint32_t t = threadIdx.x; t < kLatRing * 16 * kQuadBlocks; t += kLatThreads)
+        (&ring[0][0][0])[t * kQuadRow + kQuadLeaves] = make_uint4(1, 1, 1, 1);
     __syncthreads();
     if (producer) {
         // lane (c, j) schedules blocks j, j+8, j+16, ... of leaf c
@@ -613,7 +636,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
                 uint32_t w[16];
                 block_words(cur, w);
                 if (b + kQuadBlocks < v.nb) cur = load_block<ALIGNED>(v.p + 64 * (b + kQuadBlocks));
-                uint4* kw = &ring[0][it % kLatRing][0][j * kQuadLeaves + c];
+                uint4* kw = &ring[it % kLatRing][0][j * kQuadRow + c];
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
                     uint32_t u[4];
@@ -647,12 +670,12 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         uint32_t x[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) x[k] = role_a ? st0[k] : st0[4 + k];
-        const uint4* col = &ring[role_a ? 1 : 0][0][0][c];
+        const uint4* col = &ring[0][0][role_a ? kQuadLeaves : c];
         __syncthreads();
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
             for (uint32_t k = 0; k < kQuadBlocks; k++) {
-                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw(x, kw + k * kQuadLeaves, sh, msk, neg);
+                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw(x, kw + k * kQuadRow, sh, msk, neg);
             }
             __syncthreads();
         }

@@ -51,7 +51,7 @@ func gpu() error {
 			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
 			return
 		}
-		// every visible GPU, 2 worker slots each, 2048 leaves per batch, 2 ms linger (DESIGN.md §6.9)
+		// every visible GPU, 2 worker slots each, 4096 leaves per batch, 2 ms linger (DESIGN.md §6.9)
 		if rc := C.dm_batcher_create(nil, 0, C.DM_BATCH_PROCESS, C.uint64_t(chain.SegmentSize), C.int(chain.DataShards),
 			C.int(chain.ParShards), 0, 0, 0, 2000, &batcher); rc != C.DM_OK {
 			initEr = errors.New(C.GoString(C.dm_batcher_last_error()))

@@ -164,6 +164,22 @@ def test_batch_ragged_objects(ctx, oracle_lib, leaf_mode):
     assert [got[32 * i:32 * i + 32] for i in range(len(objs))] == wants
 
 
+def test_batch_misaligned_device_objects(ctx, oracle_lib, leaf_mode):
+    """Table mode over device objects starting at 1..15-byte offsets (unaligned loads through
+    global-address-space pointers taken from the table)."""
+    torch = _torch()
+    import random
+    rnd = random.Random(17)
+    lens = [rnd.choice([1, 55, 64, 100, 4095, 4097, 20000]) for _ in range(64)]
+    objs = [oracle_lib.splitmix_bytes(n, 3000 + i) for i, n in enumerate(lens)]
+    keep = [dev_bytes(o, offset=1 + i % 15) for i, o in enumerate(objs)]
+    out = torch.zeros(32 * len(objs), dtype=torch.uint8, device="cuda")
+    ctx.root_batch_device_async([p for _, p in keep], lens, 4096, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = bytes(out.cpu().numpy())
+    assert [got[32 * i:32 * i + 32] for i in range(len(objs))] == [oracle_lib.root_buffer(o, 4096)[1] for o in objs]
+
+
 # ---------------------------------------------------------------- edge cases
 def test_leaf_counts_sweep(ctx, oracle_lib, leaf_mode):
     """Every n in 1..600 (odd-node duplication at each level, fused K1 tiles + K2 tiles)."""
