@@ -246,11 +246,15 @@ int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
 }
 
 template <bool TABLE, bool ALIGNED>
-void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
+void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind, int cus) {
     const uint64_t n = la.nleaves;
-    if (kind == DM_LEAF_QUAD)
-        hipLaunchKernelGGL((dm::leaf_kernel_quad<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kQuadLeaves)),
-                           dim3(dm::kLatThreads), 0, s, la);
+    const dim3 qgrid((uint32_t)ceil_div(n, dm::kQuadLeaves));
+    if (kind == DM_LEAF_QUAD && qgrid.x > 2 * (uint64_t)cus) {   // > 2 workgroups per CU: compact ring
+        hipLaunchKernelGGL(dm::quad_shape_primer, dim3(4 * (uint32_t)cus), dim3(dm::kLatThreads), dm::kQuadLdsBytes, s, 0);
+        hipLaunchKernelGGL((dm::leaf_kernel_quad<TABLE, ALIGNED, true>), qgrid, dim3(dm::kLatThreads), 0, s, la);
+    }
+    else if (kind == DM_LEAF_QUAD)
+        hipLaunchKernelGGL((dm::leaf_kernel_quad<TABLE, ALIGNED, false>), qgrid, dim3(dm::kLatThreads), 0, s, la);
     else if (kind == DM_LEAF_PAIR)
         hipLaunchKernelGGL((dm::leaf_kernel_pair<TABLE, ALIGNED>), dim3((uint32_t)ceil_div(n, dm::kPairLeaves)),
                            dim3(dm::kLatThreads), 0, s, la);
@@ -262,16 +266,14 @@ void launch_leaves_t(hipStream_t s, const dm::LeafArgs& la, int kind) {
                            0, s, la);
 }
 
-// Launch the chosen leaf kernel (K1 / K1L / K1P / K1Q) over la's leaves.  (K1Q workgroups fit
-// four to a CU; padding them with dynamic LDS to force two per CU was measured to change nothing
-// at <= 4,096 leaves: the dispatcher already spreads them.)
-int launch_leaves(dm_ctx* c, hipStream_t s, const dm::LeafArgs& la, bool table, bool aligned, int kind) {
+// Launch the chosen leaf kernel (K1 / K1L / K1P / K1Q) over la's leaves on device d.
+int launch_leaves(dm_ctx* c, const Dev& d, hipStream_t s, const dm::LeafArgs& la, bool table, bool aligned, int kind) {
     if (table) {
-        if (aligned) launch_leaves_t<true, true>(s, la, kind);
-        else launch_leaves_t<true, false>(s, la, kind);
+        if (aligned) launch_leaves_t<true, true>(s, la, kind, d.cus);
+        else launch_leaves_t<true, false>(s, la, kind, d.cus);
     } else {
-        if (aligned) launch_leaves_t<false, true>(s, la, kind);
-        else launch_leaves_t<false, false>(s, la, kind);
+        if (aligned) launch_leaves_t<false, true>(s, la, kind, d.cus);
+        else launch_leaves_t<false, false>(s, la, kind, d.cus);
     }
     HIP_TRY(hipGetLastError());
     return DM_OK;
@@ -305,7 +307,7 @@ int run_tree(dm_ctx* c, Dev& d, hipStream_t s, dm::LeafArgs la, bool table, bool
     }
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    RC_TRY(launch_leaves(c, s, la, table, aligned, kind));
+    RC_TRY(launch_leaves(c, d, s, la, table, aligned, kind));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     if (L1 == 0 && leaf_dig != nullptr && leaf_dig != dst)
         HIP_TRY(hipMemcpyAsync(leaf_dig, dst, n * 32, hipMemcpyDeviceToDevice, s));
@@ -393,7 +395,7 @@ int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, cons
     la.digests = d.leaves.u8();
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    RC_TRY(launch_leaves(c, s, la, true, aligned, pick_leaf_kernel(c, d, T)));
+    RC_TRY(launch_leaves(c, d, s, la, true, aligned, pick_leaf_kernel(c, d, T)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, roots));
     if (tr) HIP_TRY(hipEventRecord(tr[2], s));
@@ -530,7 +532,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         la.base = d.data.u8();
         la.nleaves = n;
         la.byte_end = ~0ull;
-        return launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, n));
+        return launch_leaves(c, d, s, la, false, aligned, pick_leaf_kernel(c, d, n));
     }
     // striped: W bytes of every leaf per step (W multiple of 64), state carried in HBM
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
@@ -575,7 +577,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         la.byte_off = b0;
         la.byte_end = b0 + w;
         la.state = state;
-        RC_TRY(launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, n)));
+        RC_TRY(launch_leaves(c, d, s, la, false, aligned, pick_leaf_kernel(c, d, n)));
     }
     return DM_OK;
 }
@@ -963,7 +965,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
     la.nleaves = n;
     la.byte_end = ~0ull;
     la.digests = d.leaves.u8();
-    RC_TRY(launch_leaves(c, d.stream, la, true, true, pick_leaf_kernel(c, d, n)));
+    RC_TRY(launch_leaves(c, d, d.stream, la, true, true, pick_leaf_kernel(c, d, n)));
     return reduce_leaves_to_host(c, d, n, leaf_out, root);
 }
 

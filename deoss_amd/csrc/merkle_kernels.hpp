@@ -544,13 +544,18 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
 constexpr int kQuadLeaves = 8;      // leaves per workgroup (8 consumer lanes per leaf)
 constexpr int kQuadBlocks = 8;      // blocks per leaf per ring stage (one producer lane each)
 constexpr int kQuadFuseMax = 3;     // 8 leaves -> 1 node
-// LDS row of one (round group, block): K+W of the 8 leaves, then one (1,1,1,1) entry that every
-// a-triple lane reads (broadcast) as the "+1" of its -d = ~d + 1.  37 KiB per workgroup: 4
-// workgroups fit a CU's 160 KiB.
+// Two ring layouts (template COMPACT).  Wide (64 KiB, two workgroups per CU): [stage][group]
+// [block][leaf] K+W plus a same-shaped region of ones that the a-triple reads instead (its V is
+// the constant 1).  Compact (37 KiB, four per CU, for 4,097 .. 8,192 leaves): each (group, block)
+// row holds the 8 leaves' K+W and then ONE (1,1,1,1) entry that every a-triple lane reads
+// (broadcast).  Both run the same rounds; with up to two workgroups per CU the compact layout
+// measured 9 % slower in table mode (46.1 vs 42.3 ms for 4,096 x 2 MiB, cause not found: same
+// hot loop, same occupancy, insensitive to code alignment), so it is used only where it adds
+// resident leaves.
 constexpr int kQuadRow = kQuadLeaves + 1;
-constexpr int kQuadG = kQuadBlocks * kQuadRow;   // uint4 per round-group row
-constexpr size_t kQuadLdsBytes = sizeof(uint4) * kLatRing * 16 * kQuadG + 4 * 8 * kQuadLeaves + 4 * 8 * (kQuadLeaves / 2);
-static_assert(4 * kQuadLdsBytes <= (160u << 10), "four K1Q workgroups must fit a CU's LDS");
+constexpr size_t kQuadLdsBytes = sizeof(uint4) * kLatRing * 16 * kQuadBlocks * kQuadRow + 4 * 8 * kQuadLeaves +
+                                 4 * 8 * (kQuadLeaves / 2);
+static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups must fit a CU's LDS");
 
 // One round, hand-scheduled: hipcc re-associates the two DPP xors and cannot fold a bank-masked
 // DPP move into its add, so the round is written out.  H (= X7 ^ N + V, then + d on the e-triple)
@@ -576,10 +581,10 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four K1Q workgroups must fit a
 // last round of a block: the next H depends on the feed-forward, so just wait
 #define DM_QUAD_NO_NEXT "s_nop 1\n\t"
 
-// 64 rounds of one block from the ring (kw: this lane's entry, stride kQuadG per round group).
+// 64 rounds of one block from the ring (kw: this lane's entry, stride G uint4 per round group).
+template <int G>
 __device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
                                                     uint32_t neg) {
-    constexpr int G = kQuadG;
     uint32_t x4 = x[0], x5 = x[1], x6 = x[2], x7 = x[3];
     uint32_t r_, f_, s_, h;
     uint4 q = kw[0];
@@ -607,11 +612,12 @@ __device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint
     x[0] += x4; x[1] += x5; x[2] += x6; x[3] += x7;
 }
 
-template <bool TABLE, bool ALIGNED>
+template <bool TABLE, bool ALIGNED, bool COMPACT>
 __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
-    constexpr int G = kQuadG;                                 // uint4 per group row
-    // [stage][group][block][leaf 0..7 = K+W, 8 = ones]
-    __shared__ uint4 ring[kLatRing][16][G];
+    constexpr int ROW = COMPACT ? kQuadRow : kQuadLeaves;     // uint4 per (group, block) row
+    constexpr int G = kQuadBlocks * ROW;                      // uint4 per group row
+    // [region: K+W, wide layout's ones][stage][group][block][leaf (compact: + ones entry)]
+    __shared__ uint4 ring[COMPACT ? 1 : 2][kLatRing][16][G];
     __shared__ uint32_t lds_a[kQuadLeaves][8];
     __shared__ uint32_t lds_b[kQuadLeaves / 2][8];
     const uint32_t lane = threadIdx.x & 63;
@@ -623,8 +629,13 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     const LeafView v = leaf_view<TABLE>(a, i);
     const uint64_t NB = wave_max_u64(v.nb);
     const uint64_t NI = (NB + kQuadBlocks - 1) / kQuadBlocks;
-    for (uint32_t t = threadIdx.x; t < kLatRing * 16 * kQuadBlocks; t += kLatThreads)
-        (&ring[0][0][0])[t * kQuadRow + kQuadLeaves] = make_uint4(1, 1, 1, 1);
+    if constexpr (COMPACT) {
+        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * kQuadBlocks; t += kLatThreads)
+            (&ring[0][0][0][0])[t * kQuadRow + kQuadLeaves] = make_uint4(1, 1, 1, 1);
+    } else {
+        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * G; t += kLatThreads)
+            (&ring[COMPACT ? 0 : 1][0][0][0])[t] = make_uint4(1, 1, 1, 1);
+    }
     __syncthreads();
     if (producer) {
         // lane (c, j) schedules blocks j, j+8, j+16, ... of leaf c
@@ -636,7 +647,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
                 uint32_t w[16];
                 block_words(cur, w);
                 if (b + kQuadBlocks < v.nb) cur = load_block<ALIGNED>(v.p + 64 * (b + kQuadBlocks));
-                uint4* kw = &ring[it % kLatRing][0][j * kQuadRow + c];
+                uint4* kw = &ring[0][it % kLatRing][0][j * ROW + c];
 #pragma unroll
                 for (int q = 0; q < 16; q++) {
                     uint32_t u[4];
@@ -670,12 +681,12 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         uint32_t x[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) x[k] = role_a ? st0[k] : st0[4 + k];
-        const uint4* col = &ring[0][0][role_a ? kQuadLeaves : c];
+        const uint4* col = COMPACT ? &ring[0][0][0][role_a ? kQuadLeaves : c] : &ring[role_a ? 1 : 0][0][0][c];
         __syncthreads();
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
             for (uint32_t k = 0; k < kQuadBlocks; k++) {
-                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw(x, kw + k * kQuadRow, sh, msk, neg);
+                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw<G>(x, kw + k * ROW, sh, msk, neg);
             }
             __syncthreads();
         }
@@ -704,6 +715,17 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         const uint64_t o = (uint64_t)blockIdx.x * (kQuadLeaves >> a.fuse_levels) + threadIdx.x;
         store_digest(a.level_out + 32 * o, o8);
     }
+}
+
+// Empty kernel with the compact K1Q's workgroup shape (128 threads, its LDS as dynamic LDS),
+// launched just before it.  Measured on MI355X: a compact K1Q launch that directly follows a
+// kernel of another shape (e.g. K3, 256-thread workgroups) runs with fewer workgroups resident
+// -- 70.7 instead of 42.3 ms for 6,144 x 2 MiB leaves, same wave-cycles (PMC), no overlap in the
+// kernel trace -- and one 4-per-CU grid of this no-op first restores it (42.3 ms).  The cause
+// is in the dispatcher's state, not in the kernel; the primer costs microseconds.
+__global__ __launch_bounds__(kLatThreads) void quad_shape_primer(int x) {
+    extern __shared__ uint4 dyn[];
+    if (x == 12345) dyn[threadIdx.x] = make_uint4(1, 1, 1, 1);
 }
 
 // K2: tree reduce, `levels` (1..9) levels over tiles of 512 input nodes; the first level reads

@@ -115,7 +115,7 @@ int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
     la.byte_end = ~0ull;
     la.digests = bt->digests.u8();
     const int kind = pick_leaf_kernel(st->c, st->c->devs[st->dev], n);
-    launch_leaves_t<true, true>(s, la, kind);
+    launch_leaves_t<true, true>(s, la, kind, st->c->devs[st->dev].cus);
     SHIP(hipGetLastError());
     st->launched = upto;
     SHIP(hipEventRecord(st->ev_comp[k], s));

@@ -62,7 +62,7 @@ int process_segments(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t seg
     la.digests = d.leaves.u8();
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    RC_TRY(launch_leaves(c, s, la, true, true, pick_leaf_kernel(c, d, T)));
+    RC_TRY(launch_leaves(c, d, s, la, true, true, pick_leaf_kernel(c, d, T)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     if (nobj == 1) RC_TRY(finish(c, d, s, d.leaves.u8(), nseg, true, fids));
     else RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, fids));

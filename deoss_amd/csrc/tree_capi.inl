@@ -72,7 +72,7 @@ int verify_dev(dm_ctx* c, Dev& d, hipStream_t s, const void* const* contents, co
     la.nleaves = q;
     la.byte_end = ~0ull;
     la.digests = d.leaves.u8();
-    RC_TRY(launch_leaves(c, s, la, true, aligned, pick_leaf_kernel(c, d, q)));
+    RC_TRY(launch_leaves(c, d, s, la, true, aligned, pick_leaf_kernel(c, d, q)));
     hipLaunchKernelGGL(dm::verify_kernel, dim3((uint32_t)ceil_div(q, dm::kProofBlock)), dim3(dm::kProofBlock), 0, s,
                        d.leaves.u8(), paths, bits, depth, q, roots, root_stride, ok);
     HIP_TRY(hipGetLastError());
@@ -91,7 +91,7 @@ int verify_object_dev(dm_ctx* c, Dev& d, hipStream_t s, const void* dev, uint64_
     const bool aligned = is_aligned16(dev) && chunk % 16 == 0;
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    RC_TRY(launch_leaves(c, s, la, false, aligned, pick_leaf_kernel(c, d, q)));
+    RC_TRY(launch_leaves(c, d, s, la, false, aligned, pick_leaf_kernel(c, d, q)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     hipLaunchKernelGGL(dm::verify_kernel, dim3((uint32_t)ceil_div(q, dm::kProofBlock)), dim3(dm::kProofBlock), 0, s,
                        d.leaves.u8(), paths, bits, depth, q, roots, root_stride, ok);

@@ -31,3 +31,10 @@ def timed(f, reps=3):
 print("uniform+fuse", timed(lambda: ctx.root_device_async(buf.data_ptr(), n * chunk, chunk, root.data_ptr())))
 print("uniform k=0 ", timed(lambda: ctx.subtree_device_async(buf.data_ptr(), n * chunk, chunk, 0, nodes.data_ptr())))
 print("table       ", timed(lambda: ctx.root_batch_device_async(ptrs, [chunk] * n, chunk, roots.data_ptr())))
+# order check: does a uniform launch right after a batch (K3) run slow too?
+ctx.set_timing(True)
+ctx.root_batch_device_async(ptrs, [chunk] * n, chunk, roots.data_ptr())
+ctx.subtree_device_async(buf.data_ptr(), n * chunk, chunk, 0, nodes.data_ptr())
+torch.cuda.synchronize()
+print("note: per-call leaf ms after a batch:", ctx.timing_summary())
+ctx.set_timing(False)
