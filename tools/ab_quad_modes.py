@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from deoss_amd import MerkleContext
 
-n, chunk = int(sys.argv[1]) if len(sys.argv) > 1 else 4096, 2 << 20
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 2 << 20
 ctx = MerkleContext()
 buf = torch.empty(n * chunk + 64, dtype=torch.uint8, device="cuda")
 ctx.fill_synthetic_async(buf.data_ptr(), 0, n * chunk, 7)
