@@ -32,7 +32,7 @@ KERNELS = {
     "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", (1, 0)),
     "latency": ("_ZN2dm15leaf_kernel_latILb0ELb1EEEvNS_8LeafArgsE", (1, 1)),
     "pair": ("_ZN2dm16leaf_kernel_pairILb0ELb1EEEvNS_8LeafArgsE", (2, 2)),
-    "quad": ("_ZN2dm16leaf_kernel_quadILb0ELb1EEEvNS_8LeafArgsE", (8, 1)),
+    "quad": ("_ZN2dm16leaf_kernel_quadILb0ELb1ELb0EEEvNS_8LeafArgsE", (8, 1)),   # wide ring (the headline)
 }
 K1_SYMBOL = KERNELS["wide"][0]
 
