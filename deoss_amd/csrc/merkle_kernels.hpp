@@ -527,18 +527,22 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
 // K1Q: the rounds of one leaf spread over 8 lanes, for the fewest, longest leaves.  In K1P the
 // consumer wave still issues 3 rotations + an xor3 per Sigma; here each of three lanes does one
 // rotation (one v_alignbit with a per-lane shift) and two DPP xors combine them, so every lane of
-// the triple holds Sigma.  Lanes 8c+0..2 (e-triple) hold (e,f,g,h), lanes 8c+4..6 (a-triple)
-// (a,b,c,d), lanes 8c+3 / 8c+7 idle.  Per round, with per-lane constants (e / a):
+// the triple holds Sigma.  Leaf c owns two quads of one 16-lane row, 8 lanes apart: the e-triple
+// (lanes 0..2 of the quad, holding e,f,g,h) and the a-triple (a,b,c,d); lane 3 of each quad idles.
+// The a-triple runs two rounds behind the e-triple: round s of e needs d(s) = a(s-3), which the
+// a-triple finished a step earlier, and round s-2 of a needs T1(s-2) = e(s-1) - d(s-2), which the
+// e-triple finished a step earlier -- so one symmetric DPP add (row_ror:8) per step moves both,
+// off the dependent chain.  Per step, with per-lane constants (e / a):
 //   R  = rotr(X4, s)                        s = 6,11,25 / 2,13,22
 //   S  = R ^ R[q1] ^ R[q2]  (two DPP xors)  Sigma1(e) / Sigma0(a)
 //   F  = bitop3 pair of K1P                 Ch(e,f,g) / Maj(a,b,c)
-//   H' = (X7 ^ N) + V                       h + KW / -d            (N = 0 / ~0, V = KW / 1)
-//   H' += d  on the e-triple                (DPP add from lane+4, bank-masked)
-//   T  = S + F + H'                         e' = T1 + d / Sigma0 + Maj - d
-//   X4' = T (+ T[lane-4] on the a-triple)   e' / T1 + T2           (DPP add, bank-masked)
-// 9 instructions (11 issue slots) per round instead of K1P's 11 (15).  The producer wave gives
-// each of a leaf's 8 lanes its own block (8 consecutive blocks per ring stage, 512 contiguous
-// bytes per leaf per load), so one producer wave keeps up with the faster consumer.
+//   X7 = S + F + H                          e(s+1) / a(s-1)
+//   HN = (X6 ^ N) + V + X4[lane ^ 8]        next H: h + KW + d / T1 = e - d   (N = 0 / ~0, V = KW / 1)
+// 8 instructions per step, a 4-deep chain (alignbit, xor, xor, add3); 66 steps per 64-byte block.
+// The earlier lock-step form (both triples on one round, two bank-masked exchanges) took 9
+// instructions and a 5-deep chain: 669.9 -> 625.7 ms for the 8 GiB / 32 MiB headline.  The
+// producer wave gives each of a leaf's 8 lanes its own block (8 consecutive blocks per ring
+// stage, 512 contiguous bytes per leaf per load), so one producer wave keeps up with the consumer.
 // LDS: K+W ring [stage][group of 4 rounds][block][leaf] x 16 B (a producer store is 64
 // consecutive uint4; a consumer load is 8 distinct uint4, each broadcast to a leaf's lanes), and
 // a same-shaped region of ones that the a-triple reads instead (its V is the constant 1).
@@ -558,59 +562,89 @@ constexpr size_t kQuadLdsBytes = sizeof(uint4) * kLatRing * 16 * kQuadBlocks * k
                                  4 * 8 * (kQuadLeaves / 2);
 static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups must fit a CU's LDS");
 
-// One round, hand-scheduled: hipcc re-associates the two DPP xors and cannot fold a bank-masked
-// DPP move into its add, so the round is written out.  H (= X7 ^ N + V, then + d on the e-triple)
-// of the NEXT round is computed in the shadow of this round's add3; its inputs are this round's
-// X6 (next round's X7) and the next round's V.  Wait states: every DPP source VGPR is written at
-// least two instructions earlier (X4 of the rotation by the previous round's last instruction).
-#define DM_QUAD_ROUND_ASM(X4, X5, X6, X7, H, VN, TAIL)                                  \
-    asm volatile("v_alignbit_b32 %[r], %[x4], %[x4], %[sh]\n\t"                         \
-                 "v_bitop3_b32 %[f], %[x4], %[x5], %[msk] bitop3:0x1e\n\t"              \
-                 "v_bitop3_b32 %[f], %[f], %[x6], %[x5] bitop3:0xca\n\t"                \
-                 "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t" \
-                 "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t" \
-                 "v_add3_u32 %[x7], %[s], %[f], %[h]\n\t"                               \
-                 TAIL                                                                   \
-                 "v_add_u32_dpp %[x7], %[x7], %[x7] row_shr:4 row_mask:0xf bank_mask:0xa" \
-                 : [x7] "+v"(X7), [h] "+v"(H), [r] "=&v"(r_), [f] "=&v"(f_), [s] "=&v"(s_) \
-                 : [x4] "v"(X4), [x5] "v"(X5), [x6] "v"(X6), [sh] "v"(sh), [msk] "v"(msk), \
-                   [neg] "v"(neg), [vn] "v"(VN))
-// next round's H from (X6, VN)
-#define DM_QUAD_NEXT_H                                                                  \
-    "v_xad_u32 %[h], %[x6], %[neg], %[vn]\n\t"                                          \
-    "v_add_u32_dpp %[h], %[x6], %[h] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
-// last round of a block: the next H depends on the feed-forward, so just wait
-#define DM_QUAD_NO_NEXT "s_nop 1\n\t"
+// One skewed step, hand-scheduled (8 VALU): the e-triple runs round s, the a-triple round s-2.
+// H is this step's add3 term (made by the previous step), HN the next step's:
+//   HN = (X6 ^ N) + V            e: h(s+1) + KW(s+1)          a: -d(s-1)
+//   HN += X4[lane ^ 8]           e: + a(s-2) = d(s+1)         a: + e(s) = T1(s-1) + d(s-1)
+//   X7 = Sigma + F + H           e: e(s+1)                    a: a(s-1) = T1 + T2 of round s-2
+// The row_ror:8 DPP add is the whole exchange: each leaf's e-quad and a-quad sit 8 lanes apart
+// in one 16-lane row, so the same instruction hands a(s-2) to the e-triple and e(s) to the
+// a-triple.  hipcc re-associates DPP xors and cannot emit a bank-masked DPP move, so the steps are
+// written out.  Wait states: every DPP source VGPR is written at least two instructions earlier.
+#define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN)                                                   \
+    "v_alignbit_b32 %[r], %[" X4 "], %[" X4 "], %[sh]\n\t"                                      \
+    "v_bitop3_b32 %[f], %[" X4 "], %[" X5 "], %[msk] bitop3:0x1e\n\t"                          \
+    "v_xad_u32 %[" HN "], %[" X6 "], %[neg], %[" VN "]\n\t"                                     \
+    "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    "v_bitop3_b32 %[f], %[f], %[" X6 "], %[" X5 "] bitop3:0xca\n\t"                             \
+    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    "v_add_u32_dpp %[" HN "], %[" X4 "], %[" HN "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
+    "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
+// four steps; the role registers rotate through P0..P3 = a, b, c, d and H alternates h / g
+#define DM_QS_STEPS4                                                                             \
+    DM_QS_STEP("a", "b", "c", "d", "h", "g", "v0") DM_QS_STEP("d", "a", "b", "c", "g", "h", "v1") \
+    DM_QS_STEP("c", "d", "a", "b", "h", "g", "v2") DM_QS_STEP("b", "c", "d", "a", "g", "h", "v3")
+// a-quads only (banks 2, 3 of each row): P <- chain word X
+#define DM_QS_RESTORE_A(P, X) "v_mov_b32_dpp %[" P "], %[" X "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"
+// feed-forward on one lane type: X += P (bank 0x3 = e-quads, 0xc = a-quads)
+#define DM_QS_FF(X, P, BANKS) "v_add_u32_dpp %[" X "], %[" P "], %[" X "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" BANKS "\n\t"
+#define DM_QS_IN                                                                                 \
+    : [sh] "v"(sh), [msk] "v"(msk), [neg] "v"(neg), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2),     \
+      [v3] "v"(v3)
+#define DM_QS_OPS                                                                                \
+    : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "+v"(h), [g] "+v"(g),           \
+      [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),          \
+      [f] "=&v"(f_), [s] "=&v"(s_) DM_QS_IN
 
-// 64 rounds of one block from the ring (kw: this lane's entry, stride G uint4 per round group).
+// One 64-byte block from the ring: 66 skewed steps (the a-triple starts two steps late and
+// finishes two steps after the e-triple).  x = this lane's chaining words: e-triple (e,f,g,h),
+// a-triple (c,d,a,b) -- stored rotated so that both triples start from P = x and feed forward
+// x += P.  The first four steps read x where P still equals it, so P needs no copy.  The
+// a-triple's first two steps run on stale values; their writes to P3 and P2 are overwritten with
+// b and a before anything reads them, and the e-triple feeds forward after its 64th step, before
+// its own two idle steps overwrite P3 and P2.
 template <int G>
-__device__ __forceinline__ void quad_rounds_from_kw(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
-                                                    uint32_t neg) {
-    uint32_t x4 = x[0], x5 = x[1], x6 = x[2], x7 = x[3];
-    uint32_t r_, f_, s_, h;
-    uint4 q = kw[0];
-    // H of round 0: (x7 ^ N) + V, + d on the e-triple (x7 may have just been written: wait first)
+__device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
+                                                  uint32_t neg) {
+    uint32_t p0, p1, p2, p3, h, g, r_, f_, s_;
+    uint4 q = kw[0], nq = kw[G];
+    // H of step 0 as if made by step -1 (X6 = P3 = x3, X4 = P1 = x1)
     asm volatile("s_nop 1\n\t"
-                 "v_xad_u32 %[h], %[x7], %[neg], %[v]\n\t"
-                 "v_add_u32_dpp %[h], %[x7], %[h] row_shl:4 row_mask:0xf bank_mask:0x5"
+                 "v_xad_u32 %[h], %[x3], %[neg], %[v]\n\t"
+                 "v_add_u32_dpp %[h], %[x1], %[h] row_ror:8 row_mask:0xf bank_mask:0xf"
                  : [h] "=&v"(h)
-                 : [x7] "v"(x7), [neg] "v"(neg), [v] "v"(q.x));
+                 : [x3] "v"(x[3]), [x1] "v"(x[1]), [neg] "v"(neg), [v] "v"(q.x));
 #pragma unroll
-    for (int g = 0; g < 16; g++) {
-        uint4 nq = q;
-        if (g + 1 < 16) nq = kw[(g + 1) * G];
-        // register roles rotate: each round's new X4 lands in its X7 register
-        DM_QUAD_ROUND_ASM(x4, x5, x6, x7, h, q.y, DM_QUAD_NEXT_H);
-        DM_QUAD_ROUND_ASM(x7, x4, x5, x6, h, q.z, DM_QUAD_NEXT_H);
-        DM_QUAD_ROUND_ASM(x6, x7, x4, x5, h, q.w, DM_QUAD_NEXT_H);
-        if (g + 1 < 16) {
-            DM_QUAD_ROUND_ASM(x5, x6, x7, x4, h, nq.x, DM_QUAD_NEXT_H);
+    for (int grp = 0; grp < 16; grp++) {
+        // the group after next is loaded now, so its LDS latency hides behind this group's steps
+        const uint4 nnq = grp + 2 < 16 ? kw[(grp + 2) * G] : nq;
+        const uint32_t v0 = q.y, v1 = q.z, v2 = q.w, v3 = nq.x;
+        if (grp == 0) {
+            asm volatile(DM_QS_STEP("x0", "x1", "x2", "d", "h", "g", "v0") DM_QS_RESTORE_A("d", "x3")
+                         DM_QS_STEP("d", "x0", "x1", "c", "g", "h", "v1") DM_QS_RESTORE_A("c", "x2")
+                         DM_QS_STEP("c", "d", "x0", "b", "h", "g", "v2")
+                         DM_QS_STEP("b", "c", "d", "a", "g", "h", "v3")
+                         : [a] "=&v"(p0), [b] "=&v"(p1), [c] "=&v"(p2), [d] "=&v"(p3), [h] "+v"(h), [g] "=&v"(g),
+                           [r] "=&v"(r_), [f] "=&v"(f_), [s] "=&v"(s_)
+                         : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]),
+                           [sh] "v"(sh), [msk] "v"(msk), [neg] "v"(neg), [v0] "v"(v0), [v1] "v"(v1),
+                           [v2] "v"(v2), [v3] "v"(v3));
         } else {
-            DM_QUAD_ROUND_ASM(x5, x6, x7, x4, h, nq.x, DM_QUAD_NO_NEXT);
+            asm volatile(DM_QS_STEPS4 DM_QS_OPS);
         }
         q = nq;
+        nq = nnq;
     }
-    x[0] += x4; x[1] += x5; x[2] += x6; x[3] += x7;
+    {
+        // e-triple feed-forward (P0 was written last), then the a-triple's last two rounds
+        const uint32_t v0 = q.x, v1 = q.x, v2 = q.x, v3 = q.x;
+        asm volatile(DM_QS_FF("x3", "d", "0x3") DM_QS_FF("x2", "c", "0x3") DM_QS_FF("x1", "b", "0x3")
+                     DM_QS_FF("x0", "a", "0x3")
+                     DM_QS_STEP("a", "b", "c", "d", "h", "g", "v0") DM_QS_STEP("d", "a", "b", "c", "g", "h", "v1")
+                     DM_QS_FF("x0", "a", "0xc") DM_QS_FF("x1", "b", "0xc") DM_QS_FF("x3", "d", "0xc")
+                     DM_QS_FF("x2", "c", "0xc")
+                     DM_QS_OPS);
+    }
 }
 
 template <bool TABLE, bool ALIGNED, bool COMPACT>
@@ -624,7 +658,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     const uint32_t lane = threadIdx.x & 63;
     const bool producer = __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;
     const uint32_t c = lane >> 3;                             // leaf within the workgroup
-    const uint32_t j = lane & 7;                              // producer: block; consumer: role
+    const uint32_t j = lane & 7;                              // producer: block j of leaf c
     const uint64_t first = (uint64_t)blockIdx.x * kQuadLeaves;
     const uint64_t i = first + c;
     const LeafView v = leaf_view<TABLE>(a, i);
@@ -671,37 +705,41 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         }
         __syncthreads();
     } else {
-        const bool role_a = j >= 4;
-        const uint32_t p = j & 3;
+        // lanes: leaf cq's e-quad = row lanes 4*(cq&1)+0..3, its a-quad 8 lanes higher (row_ror:8)
+        const uint32_t cq = 2 * (lane >> 4) + ((lane >> 2) & 1);
+        const bool role_a = (lane >> 3) & 1;
+        const uint32_t p = lane & 3;
+        const uint64_t iq = first + cq;
+        const LeafView vq = leaf_view<TABLE>(a, iq);
         const uint32_t sh = role_a ? (p == 0 ? 2 : p == 1 ? 13 : 22) : (p == 0 ? 6 : p == 1 ? 11 : 25);
         const uint32_t msk = role_a ? 0u : ~0u;
         const uint32_t neg = role_a ? ~0u : 0u;
         uint32_t st0[8];
-        if (v.active) load_or_init_state(a, i, st0);
+        if (vq.active) load_or_init_state(a, iq, st0);
         else init_state(st0);
-        uint32_t x[4];
+        uint32_t x[4];   // e-triple (e,f,g,h); a-triple (c,d,a,b)
 #pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = role_a ? st0[k] : st0[4 + k];
-        const uint4* col = COMPACT ? &ring[0][0][0][role_a ? kQuadLeaves : c] : &ring[role_a ? 1 : 0][0][0][c];
+        for (int k = 0; k < 4; k++) x[k] = role_a ? st0[(k + 2) & 3] : st0[4 + k];
+        const uint4* col = COMPACT ? &ring[0][0][0][role_a ? kQuadLeaves : cq] : &ring[role_a ? 1 : 0][0][0][cq];
         __syncthreads();
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
             for (uint32_t k = 0; k < kQuadBlocks; k++) {
-                if (it * kQuadBlocks + k < v.nb) quad_rounds_from_kw<G>(x, kw + k * ROW, sh, msk, neg);
+                if (it * kQuadBlocks + k < vq.nb) quad_block_skewed<G>(x, kw + k * ROW, sh, msk, neg);
             }
             __syncthreads();
         }
-        // full state on lane 8c: (e,f,g,h) own, (a,b,c,d) from lane 8c+4
+        // full state on the e-quad's first lane: (a,b,c,d) from the a-quad 8 lanes up
         uint32_t st[8];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            st[k] = __shfl(x[k], (int)(lane + 4), 64);
+            st[k] = __shfl(x[(k + 2) & 3], (int)(lane + 8), 64);
             st[4 + k] = x[k];
         }
-        if (v.active && j == 0) {
-            leaf_epilogue<ALIGNED>(a, i, v, st);
+        if (vq.active && !role_a && p == 0) {
+            leaf_epilogue<ALIGNED>(a, iq, vq, st);
 #pragma unroll
-            for (int k = 0; k < 8; k++) lds_a[c][k] = st[k];
+            for (int k = 0; k < 8; k++) lds_a[cq][k] = st[k];
         }
     }
     if (a.fuse_levels == 0) return;
