@@ -235,6 +235,15 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
     return x;
 }
 
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
+
 // K1: leaf SHA-256, one lane per leaf; optionally fused with the first tree levels.
 template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void leaf_kernel(LeafArgs a) {
@@ -549,101 +558,181 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_pair(LeafArgs a) {
 constexpr int kQuadLeaves = 8;      // leaves per workgroup (8 consumer lanes per leaf)
 constexpr int kQuadBlocks = 8;      // blocks per leaf per ring stage (one producer lane each)
 constexpr int kQuadFuseMax = 3;     // 8 leaves -> 1 node
-// Two ring layouts (template COMPACT).  Wide (64 KiB, two workgroups per CU): [stage][group]
-// [block][leaf] K+W plus a same-shaped region of ones that the a-triple reads instead (its V is
-// the constant 1).  Compact (37 KiB, four per CU, for 4,097 .. 8,192 leaves): each (group, block)
-// row holds the 8 leaves' K+W and then ONE (1,1,1,1) entry that every a-triple lane reads
-// (broadcast).  Both run the same rounds; with up to two workgroups per CU the compact layout
-// measured 9 % slower in table mode (46.1 vs 42.3 ms for 4,096 x 2 MiB, cause not found: same
-// hot loop, same occupancy, insensitive to code alignment), so it is used only where it adds
-// resident leaves.
-constexpr int kQuadRow = kQuadLeaves + 1;
+// Two LDS footprints (template COMPACT), one ring layout: -(K+W) [stage][group][block][leaf].
+// Wide reserves a second, unused 32 KiB region so that at most two workgroups share a CU and the
+// dispatcher spreads them; compact (33 KiB, four per CU) is used for 4,097 .. 8,192 leaves.  The
+// lock-step K1Q needed a region of ones for its a-triple (wide) or one broadcast ones entry per
+// row (compact, 9-entry rows); the skewed step needs neither.
+constexpr int kQuadRow = kQuadLeaves;
 constexpr size_t kQuadLdsBytes = sizeof(uint4) * kLatRing * 16 * kQuadBlocks * kQuadRow + 4 * 8 * kQuadLeaves +
                                  4 * 8 * (kQuadLeaves / 2);
 static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups must fit a CU's LDS");
 
-// One skewed step, hand-scheduled (8 VALU): the e-triple runs round s, the a-triple round s-2.
-// H is this step's add3 term (made by the previous step), HN the next step's:
-//   HN = (X6 ^ N) + V            e: h(s+1) + KW(s+1)          a: -d(s-1)
-//   HN += X4[lane ^ 8]           e: + a(s-2) = d(s+1)         a: + e(s) = T1(s-1) + d(s-1)
-//   X7 = Sigma + F + H           e: e(s+1)                    a: a(s-1) = T1 + T2 of round s-2
-// The row_ror:8 DPP add is the whole exchange: each leaf's e-quad and a-quad sit 8 lanes apart
-// in one 16-lane row, so the same instruction hands a(s-2) to the e-triple and e(s) to the
-// a-triple.  hipcc re-associates DPP xors and cannot emit a bank-masked DPP move, so the steps are
-// written out.  Wait states: every DPP source VGPR is written at least two instructions earlier.
-#define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN)                                                   \
+// One skewed step, hand-scheduled (8 VALU, two of them half-rate): the e-triple runs round s,
+// the a-triple round s-2.  H is this step's add3 term (made by the previous step), HN the next
+// step's.  V = -(K+W) of round s+1 from the producer.
+//   F  = Ch / Maj                    (reads X6 before it is reused)
+//   X6 = V - X6   on the e-triple    -(h(s+1) + KW(s+1)); X6 is dead after F until the next
+//                                    step's add3 overwrites it (it is that step's X7)
+//   HN = X4[lane ^ 8] - X6           e: d(s+1) + h + KW          a: e(s) - d(s-1) = T1(s-1)
+//   X7 = Sigma + F + H               e: e(s+1)                   a: a(s-1) = T1 + T2 of round s-2
+// The row_ror:8 DPP subtract is the whole exchange: each leaf's e-quad and a-quad sit 8 lanes
+// apart in one 16-lane row, so the same instruction hands a(s-2) to the e-triple and e(s) to the
+// a-triple.  Both H instructions are full-rate DPP ops (a v_xad with a per-lane negate cost a
+// half-rate slot).  hipcc re-associates DPP xors and cannot emit bank-masked DPP ops, so the
+// steps are written out.  Wait states: every DPP source VGPR is written at least two
+// instructions earlier.
+#define DM_QS_HEAD(X4, X5, X6)                                                                   \
     "v_alignbit_b32 %[r], %[" X4 "], %[" X4 "], %[sh]\n\t"                                      \
     "v_bitop3_b32 %[f], %[" X4 "], %[" X5 "], %[msk] bitop3:0x1e\n\t"                          \
-    "v_xad_u32 %[" HN "], %[" X6 "], %[neg], %[" VN "]\n\t"                                     \
-    "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"        \
     "v_bitop3_b32 %[f], %[f], %[" X6 "], %[" X5 "] bitop3:0xca\n\t"                             \
+    "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"
+#define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN)                                                   \
+    DM_QS_HEAD(X4, X5, X6)                                                                       \
+    "v_sub_u32_dpp %[" X6 "], %[" VN "], %[" X6 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t" \
     "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
-    "v_add_u32_dpp %[" HN "], %[" X4 "], %[" HN "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
+    "v_sub_u32_dpp %[" HN "], %[" X4 "], %[" X6 "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
+    "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
+// e-triple idle next step (steps 63, 64): keep X6 (the e-triple feeds forward from it), HN only
+// matters on the a-triple
+#define DM_QS_STEP_A(X4, X5, X6, X7, H, HN)                                                     \
+    DM_QS_HEAD(X4, X5, X6)                                                                       \
+    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    "v_sub_u32_dpp %[" HN "], %[" X4 "], %[" X6 "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
+    "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
+// last step of a block: no next H
+#define DM_QS_STEP_END(X4, X5, X6, X7, H)                                                       \
+    DM_QS_HEAD(X4, X5, X6)                                                                       \
+    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
     "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
 // four steps; the role registers rotate through P0..P3 = a, b, c, d and H alternates h / g
-#define DM_QS_STEPS4                                                                             \
-    DM_QS_STEP("a", "b", "c", "d", "h", "g", "v0") DM_QS_STEP("d", "a", "b", "c", "g", "h", "v1") \
-    DM_QS_STEP("c", "d", "a", "b", "h", "g", "v2") DM_QS_STEP("b", "c", "d", "a", "g", "h", "v3")
-// a-quads only (banks 2, 3 of each row): P <- chain word X
+#define DM_QS_STEPS4V(V0, V1, V2, V3)                                                          \
+    DM_QS_STEP("a", "b", "c", "d", "h", "g", V0) DM_QS_STEP("d", "a", "b", "c", "g", "h", V1)   \
+    DM_QS_STEP("c", "d", "a", "b", "h", "g", V2) DM_QS_STEP("b", "c", "d", "a", "g", "h", V3)
+// H of step 0, as if made by step -1 (X6 = P3, X4 = P1); P may have just been copied from x
+#define DM_QS_PROLOGUE(V)                                                                        \
+    "s_nop 1\n\t"                                                                                \
+    "v_sub_u32_dpp %[d], %[" V "], %[d] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"       \
+    "v_sub_u32_dpp %[h], %[b], %[d] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+// steps 0..3: the a-triple's first two steps run on stale values; their writes to P3 and P2 are
+// replaced by b and a (a-quads only) before anything reads them
 #define DM_QS_RESTORE_A(P, X) "v_mov_b32_dpp %[" P "], %[" X "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xc\n\t"
-// feed-forward on one lane type: X += P (bank 0x3 = e-quads, 0xc = a-quads)
+#define DM_QS_GROUP0(V0, V1, V2, V3)                                                             \
+    DM_QS_STEP("a", "b", "c", "d", "h", "g", V0) DM_QS_RESTORE_A("d", "x3")                      \
+    DM_QS_STEP("d", "a", "b", "c", "g", "h", V1) DM_QS_RESTORE_A("c", "x2")                      \
+    DM_QS_STEP("c", "d", "a", "b", "h", "g", V2) DM_QS_STEP("b", "c", "d", "a", "g", "h", V3)
+// steps 60..65 and both feed-forwards: the e-triple after step 63 (P0 written last), the
+// a-triple after step 65 (P2 written last).  FF: x += P on one lane type (bank 0x3 = e-quads,
+// 0xc = a-quads).
 #define DM_QS_FF(X, P, BANKS) "v_add_u32_dpp %[" X "], %[" P "], %[" X "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:" BANKS "\n\t"
-#define DM_QS_IN                                                                                 \
-    : [sh] "v"(sh), [msk] "v"(msk), [neg] "v"(neg), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2),     \
-      [v3] "v"(v3)
-#define DM_QS_OPS                                                                                \
+#define DM_QS_TAIL(V0, V1, V2)                                                                   \
+    DM_QS_STEP("a", "b", "c", "d", "h", "g", V0) DM_QS_STEP("d", "a", "b", "c", "g", "h", V1)   \
+    DM_QS_STEP("c", "d", "a", "b", "h", "g", V2) DM_QS_STEP_A("b", "c", "d", "a", "g", "h")      \
+    DM_QS_FF("x3", "d", "0x3") DM_QS_FF("x2", "c", "0x3") DM_QS_FF("x1", "b", "0x3")             \
+    DM_QS_FF("x0", "a", "0x3")                                                                   \
+    DM_QS_STEP_A("a", "b", "c", "d", "h", "g") DM_QS_STEP_END("d", "a", "b", "c", "g")           \
+    DM_QS_FF("x0", "a", "0xc") DM_QS_FF("x1", "b", "0xc") DM_QS_FF("x3", "d", "0xc")             \
+    DM_QS_FF("x2", "c", "0xc")
+#define DM_QS_OUT                                                                                \
     : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "+v"(h), [g] "+v"(g),           \
       [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),          \
-      [f] "=&v"(f_), [s] "=&v"(s_) DM_QS_IN
+      [f] "=&v"(f_), [s] "=&v"(s_)
+#define DM_QS_OPS DM_QS_OUT : [sh] "v"(sh), [msk] "v"(msk), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3)
 
 // One 64-byte block from the ring: 66 skewed steps (the a-triple starts two steps late and
 // finishes two steps after the e-triple).  x = this lane's chaining words: e-triple (e,f,g,h),
 // a-triple (c,d,a,b) -- stored rotated so that both triples start from P = x and feed forward
-// x += P.  The first four steps read x where P still equals it, so P needs no copy.  The
-// a-triple's first two steps run on stale values; their writes to P3 and P2 are overwritten with
-// b and a before anything reads them, and the e-triple feeds forward after its 64th step, before
-// its own two idle steps overwrite P3 and P2.
-template <int G>
-__device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk,
-                                                  uint32_t neg) {
-    uint32_t p0, p1, p2, p3, h, g, r_, f_, s_;
-    uint4 q = kw[0], nq = kw[G];
-    // H of step 0 as if made by step -1 (X6 = P3 = x3, X4 = P1 = x1)
-    asm volatile("s_nop 1\n\t"
-                 "v_xad_u32 %[h], %[x3], %[neg], %[v]\n\t"
-                 "v_add_u32_dpp %[h], %[x1], %[h] row_ror:8 row_mask:0xf bank_mask:0xf"
-                 : [h] "=&v"(h)
-                 : [x3] "v"(x[3]), [x1] "v"(x[1]), [neg] "v"(neg), [v] "v"(q.x));
+// x += P.  kw(grp) gives -(K+W) of rounds 4grp..4grp+3 (an LDS read).
+template <class KW>
+__device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], KW kw, uint32_t sh, uint32_t msk) {
+    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h = 0, g = 0, r_, f_, s_;
+    uint4 q = kw(0), nq = kw(1);
+    {
+        const uint32_t v0 = q.x, v1 = 0, v2 = 0, v3 = 0;
+        asm volatile(DM_QS_PROLOGUE("v0") DM_QS_OPS);
+    }
 #pragma unroll
     for (int grp = 0; grp < 16; grp++) {
         // the group after next is loaded now, so its LDS latency hides behind this group's steps
-        const uint4 nnq = grp + 2 < 16 ? kw[(grp + 2) * G] : nq;
+        const uint4 nnq = grp + 2 < 16 ? kw(grp + 2) : nq;
         const uint32_t v0 = q.y, v1 = q.z, v2 = q.w, v3 = nq.x;
         if (grp == 0) {
-            asm volatile(DM_QS_STEP("x0", "x1", "x2", "d", "h", "g", "v0") DM_QS_RESTORE_A("d", "x3")
-                         DM_QS_STEP("d", "x0", "x1", "c", "g", "h", "v1") DM_QS_RESTORE_A("c", "x2")
-                         DM_QS_STEP("c", "d", "x0", "b", "h", "g", "v2")
-                         DM_QS_STEP("b", "c", "d", "a", "g", "h", "v3")
-                         : [a] "=&v"(p0), [b] "=&v"(p1), [c] "=&v"(p2), [d] "=&v"(p3), [h] "+v"(h), [g] "=&v"(g),
-                           [r] "=&v"(r_), [f] "=&v"(f_), [s] "=&v"(s_)
-                         : [x0] "v"(x[0]), [x1] "v"(x[1]), [x2] "v"(x[2]), [x3] "v"(x[3]),
-                           [sh] "v"(sh), [msk] "v"(msk), [neg] "v"(neg), [v0] "v"(v0), [v1] "v"(v1),
-                           [v2] "v"(v2), [v3] "v"(v3));
+            asm volatile(DM_QS_GROUP0("v0", "v1", "v2", "v3") DM_QS_OPS);
+        } else if (grp < 15) {
+            asm volatile(DM_QS_STEPS4V("v0", "v1", "v2", "v3") DM_QS_OPS);
         } else {
-            asm volatile(DM_QS_STEPS4 DM_QS_OPS);
+            asm volatile(DM_QS_TAIL("v0", "v1", "v2") DM_QS_OPS);
         }
         q = nq;
         nq = nnq;
     }
-    {
-        // e-triple feed-forward (P0 was written last), then the a-triple's last two rounds
-        const uint32_t v0 = q.x, v1 = q.x, v2 = q.x, v3 = q.x;
-        asm volatile(DM_QS_FF("x3", "d", "0x3") DM_QS_FF("x2", "c", "0x3") DM_QS_FF("x1", "b", "0x3")
-                     DM_QS_FF("x0", "a", "0x3")
-                     DM_QS_STEP("a", "b", "c", "d", "h", "g", "v0") DM_QS_STEP("d", "a", "b", "c", "g", "h", "v1")
-                     DM_QS_FF("x0", "a", "0xc") DM_QS_FF("x1", "b", "0xc") DM_QS_FF("x3", "d", "0xc")
-                     DM_QS_FF("x2", "c", "0xc")
-                     DM_QS_OPS);
+}
+
+constexpr int kLgkmWait0 = 0xC07F;   // s_waitcnt lgkmcnt(0), no wait on vmcnt / expcnt (gfx9 encoding)
+
+// quad_block_skewed with the block's 64 words of -(K+W) in registers: the whole block is one asm
+// statement (hipcc puts an s_nop between consecutive asm statements that share registers).
+__device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[16], uint32_t sh, uint32_t msk) {
+    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h, g, r_, f_, s_;
+    asm volatile(DM_QS_PROLOGUE("k0")
+                 DM_QS_GROUP0("k1", "k2", "k3", "k4")
+                 DM_QS_STEPS4V("k5", "k6", "k7", "k8")
+                 DM_QS_STEPS4V("k9", "k10", "k11", "k12")
+                 DM_QS_STEPS4V("k13", "k14", "k15", "k16")
+                 DM_QS_STEPS4V("k17", "k18", "k19", "k20")
+                 DM_QS_STEPS4V("k21", "k22", "k23", "k24")
+                 DM_QS_STEPS4V("k25", "k26", "k27", "k28")
+                 DM_QS_STEPS4V("k29", "k30", "k31", "k32")
+                 DM_QS_STEPS4V("k33", "k34", "k35", "k36")
+                 DM_QS_STEPS4V("k37", "k38", "k39", "k40")
+                 DM_QS_STEPS4V("k41", "k42", "k43", "k44")
+                 DM_QS_STEPS4V("k45", "k46", "k47", "k48")
+                 DM_QS_STEPS4V("k49", "k50", "k51", "k52")
+                 DM_QS_STEPS4V("k53", "k54", "k55", "k56")
+                 DM_QS_STEPS4V("k57", "k58", "k59", "k60")
+                 DM_QS_TAIL("k61", "k62", "k63")
+                 : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "=&v"(h), [g] "=&v"(g),
+                   [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),
+                   [f] "=&v"(f_), [s] "=&v"(s_)
+                 : [sh] "v"(sh), [msk] "v"(msk),
+                   [k0] "v"(K[0].x), [k1] "v"(K[0].y), [k2] "v"(K[0].z), [k3] "v"(K[0].w),
+                   [k4] "v"(K[1].x), [k5] "v"(K[1].y), [k6] "v"(K[1].z), [k7] "v"(K[1].w),
+                   [k8] "v"(K[2].x), [k9] "v"(K[2].y), [k10] "v"(K[2].z), [k11] "v"(K[2].w),
+                   [k12] "v"(K[3].x), [k13] "v"(K[3].y), [k14] "v"(K[3].z), [k15] "v"(K[3].w),
+                   [k16] "v"(K[4].x), [k17] "v"(K[4].y), [k18] "v"(K[4].z), [k19] "v"(K[4].w),
+                   [k20] "v"(K[5].x), [k21] "v"(K[5].y), [k22] "v"(K[5].z), [k23] "v"(K[5].w),
+                   [k24] "v"(K[6].x), [k25] "v"(K[6].y), [k26] "v"(K[6].z), [k27] "v"(K[6].w),
+                   [k28] "v"(K[7].x), [k29] "v"(K[7].y), [k30] "v"(K[7].z), [k31] "v"(K[7].w),
+                   [k32] "v"(K[8].x), [k33] "v"(K[8].y), [k34] "v"(K[8].z), [k35] "v"(K[8].w),
+                   [k36] "v"(K[9].x), [k37] "v"(K[9].y), [k38] "v"(K[9].z), [k39] "v"(K[9].w),
+                   [k40] "v"(K[10].x), [k41] "v"(K[10].y), [k42] "v"(K[10].z), [k43] "v"(K[10].w),
+                   [k44] "v"(K[11].x), [k45] "v"(K[11].y), [k46] "v"(K[11].z), [k47] "v"(K[11].w),
+                   [k48] "v"(K[12].x), [k49] "v"(K[12].y), [k50] "v"(K[12].z), [k51] "v"(K[12].w),
+                   [k52] "v"(K[13].x), [k53] "v"(K[13].y), [k54] "v"(K[13].z), [k55] "v"(K[13].w),
+                   [k56] "v"(K[14].x), [k57] "v"(K[14].y), [k58] "v"(K[14].z), [k59] "v"(K[14].w),
+                   [k60] "v"(K[15].x), [k61] "v"(K[15].y), [k62] "v"(K[15].z), [k63] "v"(K[15].w));
+}
+
+// One ring stage (8 blocks) when every leaf of the wave has all 8: each block's 64 K+W words go
+// to registers in one burst while the previous block runs (one s_waitcnt per block instead of
+// one per 4 rounds), and no per-block branch.
+template <int G, int ROW>
+__device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk) {
+    uint4 A[16], B[16];
+#pragma unroll
+    for (int g = 0; g < 16; g++) A[g] = kw[g * G];
+#pragma unroll
+    for (int k = 0; k < kQuadBlocks; k += 2) {
+        __builtin_amdgcn_s_waitcnt(kLgkmWait0);
+#pragma unroll
+        for (int g = 0; g < 16; g++) B[g] = kw[(k + 1) * ROW + g * G];
+        quad_block_regs(x, A, sh, msk);
+        __builtin_amdgcn_s_waitcnt(kLgkmWait0);
+        if (k + 2 < kQuadBlocks) {
+#pragma unroll
+            for (int g = 0; g < 16; g++) A[g] = kw[(k + 2) * ROW + g * G];
+        }
+        quad_block_regs(x, B, sh, msk);
     }
 }
 
@@ -651,7 +740,10 @@ template <bool TABLE, bool ALIGNED, bool COMPACT>
 __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     constexpr int ROW = COMPACT ? kQuadRow : kQuadLeaves;     // uint4 per (group, block) row
     constexpr int G = kQuadBlocks * ROW;                      // uint4 per group row
-    // [region: K+W, wide layout's ones][stage][group][block][leaf (compact: + ones entry)]
+    // -(K+W) [stage][group][block][leaf (compact: + one unused entry)].  The wide layout reserves a
+    // second, unused region: 64 KiB caps it at two workgroups per CU, so the dispatcher spreads
+    // them (at 32 KiB it packed four on some CUs and none on others: 4,096 x 4 MiB measured
+    // 96.6 instead of 65.4 ms).
     __shared__ uint4 ring[COMPACT ? 1 : 2][kLatRing][16][G];
     __shared__ uint32_t lds_a[kQuadLeaves][8];
     __shared__ uint32_t lds_b[kQuadLeaves / 2][8];
@@ -664,14 +756,6 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     const LeafView v = leaf_view<TABLE>(a, i);
     const uint64_t NB = wave_max_u64(v.nb);
     const uint64_t NI = (NB + kQuadBlocks - 1) / kQuadBlocks;
-    if constexpr (COMPACT) {
-        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * kQuadBlocks; t += kLatThreads)
-            (&ring[0][0][0][0])[t * kQuadRow + kQuadLeaves] = make_uint4(1, 1, 1, 1);
-    } else {
-        for (uint32_t t = threadIdx.x; t < kLatRing * 16 * G; t += kLatThreads)
-            (&ring[COMPACT ? 0 : 1][0][0][0])[t] = make_uint4(1, 1, 1, 1);
-    }
-    __syncthreads();
     if (producer) {
         // lane (c, j) schedules blocks j, j+8, j+16, ... of leaf c
         Blk cur;
@@ -696,7 +780,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
                             wt = ssig1(w[(t - 2) & 15]) + w[(t - 7) & 15] + ssig0(w[(t - 15) & 15]) + w[t & 15];
                             w[t & 15] = wt;
                         }
-                        u[k] = kSha256K[t] + wt;
+                        u[k] = 0u - (kSha256K[t] + wt);   // the consumer subtracts it
                     }
                     kw[q * G] = make_uint4(u[0], u[1], u[2], u[3]);
                 }
@@ -713,19 +797,26 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         const LeafView vq = leaf_view<TABLE>(a, iq);
         const uint32_t sh = role_a ? (p == 0 ? 2 : p == 1 ? 13 : 22) : (p == 0 ? 6 : p == 1 ? 11 : 25);
         const uint32_t msk = role_a ? 0u : ~0u;
-        const uint32_t neg = role_a ? ~0u : 0u;
         uint32_t st0[8];
         if (vq.active) load_or_init_state(a, iq, st0);
         else init_state(st0);
         uint32_t x[4];   // e-triple (e,f,g,h); a-triple (c,d,a,b)
 #pragma unroll
         for (int k = 0; k < 4; k++) x[k] = role_a ? st0[(k + 2) & 3] : st0[4 + k];
-        const uint4* col = COMPACT ? &ring[0][0][0][role_a ? kQuadLeaves : cq] : &ring[role_a ? 1 : 0][0][0][cq];
+        const uint4* col = &ring[0][0][0][cq];   // the a-triple reads it too (and ignores it)
         __syncthreads();
+        // blocks every leaf of this wave has (inactive leaves do not count)
+        const uint64_t nb_all = wave_min_u64(vq.active ? vq.nb : ~0ull);
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
-            for (uint32_t k = 0; k < kQuadBlocks; k++) {
-                if (it * kQuadBlocks + k < vq.nb) quad_block_skewed<G>(x, kw + k * ROW, sh, msk, neg);
+            if ((it + 1) * kQuadBlocks <= nb_all) {
+                quad_stage_regs<G, ROW>(x, kw, sh, msk);
+            } else {
+                for (uint32_t k = 0; k < kQuadBlocks; k++) {
+                    const uint4* kb = kw + k * ROW;
+                    if (it * kQuadBlocks + k < vq.nb)
+                        quad_block_skewed(x, [kb](int g) { return kb[g * G]; }, sh, msk);
+                }
             }
             __syncthreads();
         }

@@ -6,7 +6,9 @@ assembly and counts the instructions of one 64-byte block:
 
 * ``wide`` (K1, one lane per leaf): the loop streaming 4 x global_load_dwordx4 per block;
 * ``latency`` (K1L) and ``pair`` (K1P): the consumer loop (16 ds_read_b128 of K+W per block)
-  and the producer loop (16 ds_write_b128 per block).
+  and the producer loop (16 ds_write_b128 per block);
+* ``quad`` (K1Q): the consumer's whole-stage loop (8 blocks from registers, 128 ds_read_b128)
+  and the producer loop.
 
 ``lanes`` converts wave-instruction counts into lane-slots per leaf-block: K1 runs one lane per
 leaf; per leaf-block K1L spends one consumer + one producer lane, K1P two + two, K1Q eight
@@ -26,7 +28,7 @@ COUNTS = os.path.join(HERE, "isa_counts.json")
 # Issue slots per wave64 instruction relative to v_add_u32, measured on MI355X by
 # tools/valu_peak.hip (profiles/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
 # the v_add_u32 / v_bitop3_b32 rate.
-SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0}
+SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0, "v_xad_u32": 2.0}
 # name: (symbol, (consumer lanes, producer lanes) per leaf-block)
 KERNELS = {
     "wide": ("_ZN2dm11leaf_kernelILb0ELb1EEEvNS_8LeafArgsE", (1, 0)),
@@ -106,6 +108,14 @@ def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
 
 def analyse_split(asm: str, sym: str) -> dict:
     loops = list(_loops(_function_body(asm, sym)))
+    # K1Q runs whole ring stages (8 blocks, 128 ds_read_b128) from registers when every leaf of
+    # the wave has them: that loop is the bench path; otherwise the per-block loop (16 reads)
+    stage = _smallest(loops, lambda l: sum(x.startswith("ds_read_b128") for x in l) >= 128)
+    if stage is not None:
+        prod = _smallest(loops, lambda l: sum(x.startswith("ds_write_b128") for x in l) >= 16)
+        if prod is None:
+            raise ValueError(f"{sym}: producer loop not found")
+        return {"consumer": _summary(stage, 8), "producer": _summary(prod, 1)}
     cons = _smallest(loops, lambda l: sum(x.startswith("ds_read_b128") for x in l) >= 16)
     prod = _smallest(loops, lambda l: sum(x.startswith("ds_write_b128") for x in l) >= 16)
     if cons is None or prod is None:
