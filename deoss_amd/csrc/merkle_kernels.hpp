@@ -609,9 +609,20 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
 #define DM_QS_STEPS4V(V0, V1, V2, V3)                                                          \
     DM_QS_STEP("a", "b", "c", "d", "h", "g", V0) DM_QS_STEP("d", "a", "b", "c", "g", "h", V1)   \
     DM_QS_STEP("c", "d", "a", "b", "h", "g", V2) DM_QS_STEP("b", "c", "d", "a", "g", "h", V3)
+// Every K1Q step instruction is 8 bytes, and where the stream sits mod 8 changes the rate.
+// Measured on MI355X with one s_nop 0 shifted in front of otherwise identical code: a stream at
+// addresses = 0 mod 8 runs the wide (<= 2 workgroups per CU) launch at 15.84 GiB/s (256 leaves)
+// and the compact (4 per CU) launch at 320 GiB/s (8,192 leaves); at 4 mod 8 the wide launch
+// drops to 12.85 and the compact one rises to 368 (reproducible over every odd and even shift,
+// profiles/r01f_align_ab.log).  So each step stream is pinned: 8-byte aligned, plus one 4-byte
+// s_nop for the compact kernel (MIS).  Cause not isolated (instruction fetch / issue arbitration
+// between the two waves sharing a SIMD in the compact case).
+#define DM_QS_ALIGN ".p2align 3\n\t"
+#define DM_QS_ALIGN_MIS ".p2align 3\n\t.if %[mis]\n\ts_nop 0\n\t.endif\n\t"
+#define DM_QS_PROLOGUE(V) DM_QS_PROLOGUE_AT(V, DM_QS_ALIGN)
 // H of step 0, as if made by step -1 (X6 = P3, X4 = P1); P may have just been copied from x
-#define DM_QS_PROLOGUE(V)                                                                        \
-    "s_nop 1\n\t"                                                                                \
+#define DM_QS_PROLOGUE_AT(V, ALIGN)                                                               \
+    "s_nop 1\n\t" ALIGN                                                                          \
     "v_sub_u32_dpp %[d], %[" V "], %[d] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"       \
     "v_sub_u32_dpp %[h], %[b], %[d] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
 // steps 0..3: the a-triple's first two steps run on stale values; their writes to P3 and P2 are
@@ -657,11 +668,11 @@ __device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], KW kw, uint3
         const uint4 nnq = grp + 2 < 16 ? kw(grp + 2) : nq;
         const uint32_t v0 = q.y, v1 = q.z, v2 = q.w, v3 = nq.x;
         if (grp == 0) {
-            asm volatile(DM_QS_GROUP0("v0", "v1", "v2", "v3") DM_QS_OPS);
+            asm volatile(DM_QS_ALIGN DM_QS_GROUP0("v0", "v1", "v2", "v3") DM_QS_OPS);
         } else if (grp < 15) {
-            asm volatile(DM_QS_STEPS4V("v0", "v1", "v2", "v3") DM_QS_OPS);
+            asm volatile(DM_QS_ALIGN DM_QS_STEPS4V("v0", "v1", "v2", "v3") DM_QS_OPS);
         } else {
-            asm volatile(DM_QS_TAIL("v0", "v1", "v2") DM_QS_OPS);
+            asm volatile(DM_QS_ALIGN DM_QS_TAIL("v0", "v1", "v2") DM_QS_OPS);
         }
         q = nq;
         nq = nnq;
@@ -672,9 +683,10 @@ constexpr int kLgkmWait0 = 0xC07F;   // s_waitcnt lgkmcnt(0), no wait on vmcnt /
 
 // quad_block_skewed with the block's 64 words of -(K+W) in registers: the whole block is one asm
 // statement (hipcc puts an s_nop between consecutive asm statements that share registers).
+template <bool MIS>
 __device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[16], uint32_t sh, uint32_t msk) {
     uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h, g, r_, f_, s_;
-    asm volatile(DM_QS_PROLOGUE("k0")
+    asm volatile(DM_QS_PROLOGUE_AT("k0", DM_QS_ALIGN_MIS)
                  DM_QS_GROUP0("k1", "k2", "k3", "k4")
                  DM_QS_STEPS4V("k5", "k6", "k7", "k8")
                  DM_QS_STEPS4V("k9", "k10", "k11", "k12")
@@ -694,7 +706,7 @@ __device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&
                  : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "=&v"(h), [g] "=&v"(g),
                    [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),
                    [f] "=&v"(f_), [s] "=&v"(s_)
-                 : [sh] "v"(sh), [msk] "v"(msk),
+                 : [mis] "i"(MIS ? 1 : 0), [sh] "v"(sh), [msk] "v"(msk),
                    [k0] "v"(K[0].x), [k1] "v"(K[0].y), [k2] "v"(K[0].z), [k3] "v"(K[0].w),
                    [k4] "v"(K[1].x), [k5] "v"(K[1].y), [k6] "v"(K[1].z), [k7] "v"(K[1].w),
                    [k8] "v"(K[2].x), [k9] "v"(K[2].y), [k10] "v"(K[2].z), [k11] "v"(K[2].w),
@@ -716,7 +728,7 @@ __device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&
 // One ring stage (8 blocks) when every leaf of the wave has all 8: each block's 64 K+W words go
 // to registers in one burst while the previous block runs (one s_waitcnt per block instead of
 // one per 4 rounds), and no per-block branch.
-template <int G, int ROW>
+template <int G, int ROW, bool MIS>
 __device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk) {
     uint4 A[16], B[16];
 #pragma unroll
@@ -726,13 +738,13 @@ __device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* k
         __builtin_amdgcn_s_waitcnt(kLgkmWait0);
 #pragma unroll
         for (int g = 0; g < 16; g++) B[g] = kw[(k + 1) * ROW + g * G];
-        quad_block_regs(x, A, sh, msk);
+        quad_block_regs<MIS>(x, A, sh, msk);
         __builtin_amdgcn_s_waitcnt(kLgkmWait0);
         if (k + 2 < kQuadBlocks) {
 #pragma unroll
             for (int g = 0; g < 16; g++) A[g] = kw[(k + 2) * ROW + g * G];
         }
-        quad_block_regs(x, B, sh, msk);
+        quad_block_regs<MIS>(x, B, sh, msk);
     }
 }
 
@@ -810,7 +822,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
             if ((it + 1) * kQuadBlocks <= nb_all) {
-                quad_stage_regs<G, ROW>(x, kw, sh, msk);
+                quad_stage_regs<G, ROW, COMPACT>(x, kw, sh, msk);
             } else {
                 for (uint32_t k = 0; k < kQuadBlocks; k++) {
                     const uint4* kb = kw + k * ROW;
