@@ -1,3 +1,4 @@
+# usage: bash tools/ab_builds.sh base exp ...  (each name = build_variants/<name>.so, built with hipcc from a patched tree)
 # A/B library builds (build_variants/*.so) on the K1Q wide (32 MiB chunks) and compact (1 MiB)
 # launches and on table-mode batches (4096 x 4 MiB: wide, 6144 x 2 MiB: compact)
 set -e
