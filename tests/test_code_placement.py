@@ -24,7 +24,9 @@ TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
 def _disassemble(tmp_path):
     fat = tmp_path / "fat.bin"
     elf = tmp_path / "gfx950.elf"
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB], check=True)
+    # -O binary with an explicit output file: objcopy without one rewrites its input in place,
+    # which corrupts the library under any process that has it mapped
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", LIB, str(fat)], check=True)
     subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fat}",
                     f"--targets={TARGET}", f"--output={elf}"], check=True)
     out = subprocess.run([f"{LLVM}/llvm-objdump", "-d", str(elf)], check=True,
