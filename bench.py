@@ -69,7 +69,12 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--object-gib", type=float, default=8.0, help="object bytes per GPU (GiB)")
+    ap.add_argument("--object-gib", type=float, default=8.0, help="object bytes per GPU (GiB), weak scaling")
+    ap.add_argument("--total-gib", type=float, default=0.0,
+                    help="object bytes across all ranks (GiB); 1024 at --gpus 8 = BASELINE configs[3] "
+                         "(1 TiB, 128 GiB per rank); 0 = --object-gib per GPU")
+    ap.add_argument("--prefix-gib", type=float, default=64.0,
+                    help="N>1 parity: sharded root vs single-GPU root of a prefix of at most this size")
     ap.add_argument("--chunk", type=int, default=32 << 20, help="chunk (leaf) bytes; default 32 MiB")
     ap.add_argument("--sweep", action="store_true", help="also run the chunk-size sweep (N=1)")
     ap.add_argument("--no-sweep", action="store_true", help=argparse.SUPPRESS)
@@ -77,10 +82,14 @@ def main() -> None:
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
-    ap.add_argument("--workload", default="object", choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent"],
+    ap.add_argument("--workload", default="object",
+                    choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files",
+                             "plumbing"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
-                         "upload: one object fed in pieces through dm_stream (hash while receiving)")
+                         "upload: one object fed in pieces through dm_stream (hash while receiving); "
+                         "files: NewHashTree(chunkPath) over --objects files of --object-mib from the page cache; "
+                         "plumbing: BASELINE configs[0], one 64 MiB object at 32 MiB chunks")
     ap.add_argument("--piece-kib", type=int, default=1024, help="upload: bytes per dm_stream_write (KiB)")
     ap.add_argument("--segment-mib", type=int, default=32, help="rs: segment bytes (chain.SegmentSize)")
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
@@ -122,6 +131,10 @@ def main() -> None:
 
     if args.workload == "upload":
         return run_upload(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "files":
+        return run_files(args, torch, dist, world, rank, device, dev_index, gloo)
+    if args.workload == "plumbing":
+        return run_plumbing(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload == "rs":
         return run_rs(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload == "process":
@@ -132,9 +145,8 @@ def main() -> None:
         return run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo)
     if args.workload != "object":
         return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
-    per_gpu = int(args.object_gib * (1 << 30))
     chunk = args.chunk
-    total = per_gpu * world
+    total = int(args.total_gib * (1 << 30)) if args.total_gib else int(args.object_gib * (1 << 30)) * world
     plan = plan_shards(total, chunk, world)
     b0, b1 = plan.byte_range(rank)
     local_len = b1 - b0
@@ -191,6 +203,9 @@ def main() -> None:
     root_hex = bytes(root_dev.cpu().numpy()).hex() if rank == 0 else None
 
     value = total * args.steps / elapsed / (1 << 30)
+    if world > 1:   # the whole-object buffer is released before the parity legs allocate theirs
+        del buf
+        torch.cuda.empty_cache()
     k1_avg_ms = k1_ms_sum / max(ncalls, 1)
     k1_bytes = local_len + 32 * ((local_len + chunk - 1) // chunk)   # read N once + 32 B per leaf
     achieved_gbs = k1_bytes / (k1_avg_ms * 1e-3) / 1e9 if k1_avg_ms > 0 else 0.0
@@ -205,22 +220,29 @@ def main() -> None:
                    "pair": "leaf_kernel_pair (K1P, producer/consumer, rounds on lane pairs)",
                    "quad": "leaf_kernel_quad (K1Q, producer/consumer, rounds spread over 8 lanes)"}[kind]
 
+    gib = total / (1 << 30)
+    if world == 1 and total == 8 << 30 and chunk == 32 << 20:
+        tag = "BASELINE configs[1]"
+    elif total == 1 << 40 and chunk == 32 << 20:
+        tag = "BASELINE configs[3] (1 TiB object" + (", 8 GPUs)" if world == 8 else f", {world} ranks)")
+    else:
+        tag = "configs[1] shape per GPU, weak scaling" if not args.total_gib else "fixed total object"
     out = {
         "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling",
         "value": round(value, 4),
         "unit": "GiB/s",
-        "n_gpus": world,
+        "n_gpus": 1 if args.same_device else world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_gib else "weak",
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic: splitmix64 bytes generated in HBM (same generator as the CPU oracle)",
         "config": {
-            "workload": f"1 object of {args.object_gib:g} GiB per GPU ({total} B total), chunk {chunk} B "
-                        f"({plan.n_leaves} leaves) - BASELINE configs[1] at N=1, configs[3] shape at N=8",
+            "workload": f"{tag}: 1 object of {gib:g} GiB ({total} B) in {world} chunk-range shard(s) of "
+                        f"{local_len / (1 << 30):g} GiB, chunk {chunk} B ({plan.n_leaves} leaves)",
             "object_bytes": total, "chunk": chunk, "leaves": plan.n_leaves,
             "parallelism": f"chunk-range shards (2^{plan.k} leaves per block), 1 process per GPU, "
                            f"RCCL all-gather of subtree roots" if world > 1 else "single GPU",
@@ -247,24 +269,215 @@ def main() -> None:
         "root": root_hex,
     }
 
+    if args.same_device:
+        out["ranks"] = world
+        out["same_device"] = True
+        out["note"] = "rehearsal: every rank on cuda:0 of one GPU; not a multi-GPU result"
     if world == 1 and rank == 0:
         extras(args, ctx, torch, buf, local_len, chunk, root_hex, out, sptr)
-    if world > 1 and rank == 0 and not args.no_verify:
-        # untimed: the sharded root must equal the single-GPU root of the whole object
-        del buf
-        full = torch.empty(total + 64, dtype=torch.uint8, device=device)
-        ctx.fill_synthetic_async(full.data_ptr(), 0, (total + 7) // 8 * 8, SEED, sptr)
-        one = torch.zeros(32, dtype=torch.uint8, device=device)
-        ctx.root_device_async(full.data_ptr(), total, chunk, one.data_ptr(), 0, sptr)
-        torch.cuda.synchronize()
-        single = bytes(one.cpu().numpy()).hex()
-        out["parity"] = {"sharded_root": root_hex, "single_gpu_root": single, "bit_exact": single == root_hex}
-        del full
+        par = out.get("cpu_baseline", {}).get("parallel")
+        if par and par.get("value"):
+            out["vs_baseline"] = round(value / par["value"], 4)
+            out["vs_baseline_basis"] = (f"GPU value / the {par['cores']}-thread CPU restatement on this host, same "
+                                        "object, same run (BASELINE.md publishes no reference number)")
+    if world > 1 and not args.no_verify:
+        out["parity"] = multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, chunk,
+                                          root_hex, barrier, gloo)
+        cpu = out["parity"].get("cpu_root_gibs")
+        if rank == 0 and cpu:
+            out["vs_baseline"] = round(value / cpu, 4)
+            out["vs_baseline_basis"] = (f"GPU value / the {out['parity']['cpu_threads']}-thread CPU restatement "
+                                        "over the same synthetic object (regenerated leaf by leaf), same run")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, chunk, root_hex, barrier, gloo):
+    """Untimed N>1 checks that fit any object size:
+    1. prefix: the sharded path over a prefix of <= --prefix-gib (the whole object when it fits)
+       vs a single-GPU root of the same prefix on rank 0;
+    2. CPU: the oracle's N-thread root of the WHOLE object, its bytes regenerated leaf by leaf on
+       the host (no whole-object buffer anywhere: 1 TiB fits)."""
+    from deoss_amd import plan_shards
+    from deoss_amd.sharding import parity_prefix, sharded_root
+    res = {"sharded_root": root_hex}
+    prefix = parity_prefix(total, chunk, int(args.prefix_gib * (1 << 30)))
+    if prefix == total:
+        sharded_prefix = root_hex      # the timed result itself
+    else:
+        pplan = plan_shards(prefix, chunk, world)
+        p0, p1 = pplan.byte_range(rank)
+        pbuf = torch.empty(max(p1 - p0, 8) + 64, dtype=torch.uint8, device=device)
+        if p1 > p0:
+            ctx.fill_synthetic_async(pbuf.data_ptr(), p0, (p1 - p0 + 7) // 8 * 8, SEED, sptr)
+        pnodes = torch.zeros(max(pplan.node_count(rank), 1) * 32, dtype=torch.uint8, device=device)
+        proot = torch.zeros(32, dtype=torch.uint8, device=device)
+
+        def sub(k):
+            if p1 > p0:
+                ctx.subtree_device_async(pbuf.data_ptr(), p1 - p0, chunk, k, pnodes.data_ptr(), sptr)
+            return pnodes
+
+        def fin(nodes, n, min_one):
+            ctx.finish_device_async(nodes.data_ptr(), n, min_one, proot.data_ptr(), sptr)
+            return proot
+        sharded_root(pplan, rank, sub, fin, torch, dist, device, comm_device="cpu" if gloo else None)
+        torch.cuda.synchronize()
+        sharded_prefix = bytes(proot.cpu().numpy()).hex() if rank == 0 else None
+        del pbuf
+        torch.cuda.empty_cache()
+    barrier()
+    if rank == 0:
+        full = torch.empty(prefix + 64, dtype=torch.uint8, device=device)
+        ctx.fill_synthetic_async(full.data_ptr(), 0, (prefix + 7) // 8 * 8, SEED, sptr)
+        one = torch.zeros(32, dtype=torch.uint8, device=device)
+        ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
+        torch.cuda.synchronize()
+        single = bytes(one.cpu().numpy()).hex()
+        del full
+        torch.cuda.empty_cache()
+        res.update({"prefix_bytes": prefix, "prefix_sharded_root": sharded_prefix, "prefix_single_gpu_root": single,
+                    "prefix_bit_exact": single == sharded_prefix})
+        ok = single == sharded_prefix
+        if not args.no_cpu:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            from oracle import Oracle
+            threads = max(1, min(os.cpu_count() or 1, 16 * (1 if args.same_device else world)))   # box CPU share
+            t0 = time.perf_counter()
+            _, cr = Oracle().root_synthetic(total, chunk, SEED, nthreads=threads)
+            dt = time.perf_counter() - t0
+            res.update({"cpu_root": cr.hex(), "cpu_threads": threads, "cpu_seconds": round(dt, 3),
+                        "cpu_root_gibs": round(total / dt / (1 << 30), 4),
+                        "cpu_bit_exact": cr.hex() == root_hex})
+            ok = ok and cr.hex() == root_hex
+        res["bit_exact"] = ok
+    barrier()
+    return res
+
+
+def golden_case(name):
+    with open(os.path.join(ROOT, "tests", "golden", "merkle_golden.json")) as f:
+        return next(c for c in json.load(f)["cases"] if c["name"] == name)
+
+
+def run_files(args, torch, dist, world, rank, device, dev_index, gloo):
+    """The reference's own entry point, NewHashTree(chunkPath) (common/hashtree/types.go:19-39):
+    --objects files of --object-mib each, already in the page cache (DeOSS writes segment files
+    and hashes them right after).  File i holds bytes [i*S, (i+1)*S) of the configs[1] synthetic
+    object, so 256 x 32 MiB files give the configs[1] root (tests/golden fixture).  One step =
+    dm_new_hash_tree (open + fstat, parallel pread into pinned staging, H2D overlapped with the
+    reads and the leaf kernel, tree, root and leaf digests back)."""
+    import shutil
+    import tempfile
+    from deoss_amd import MerkleContext
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    nfiles = args.objects if args.objects != 4096 else 256     # bench default: 256 x 32 MiB = 8 GiB
+    size = int(args.object_mib * (1 << 20)) if args.object_mib != 4.0 else 32 << 20
+    total = nfiles * size
+    orc = Oracle()
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > 2 * total else None
+    d = tempfile.mkdtemp(prefix="deoss_files_", dir=base)
+    try:
+        buf = torch.empty(size, dtype=torch.uint8)
+        paths = []
+        for i in range(nfiles):
+            orc.fill_splitmix_ptr(buf.data_ptr(), i * size, size // 8 * 8, SEED)
+            p = os.path.join(d, f"seg{i:05d}")
+            buf.numpy().tofile(p)
+            paths.append(p)
+        del buf
+        ctx = MerkleContext(devices=[dev_index])
+        ctx.set_leaf_kernel(args.leaf_kernel)
+        for _ in range(args.warmup):
+            ctx.new_hash_tree(paths)
+        times = []
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            leaves, root = ctx.new_hash_tree(paths)
+            times.append(time.perf_counter() - t0)
+        tavg = sum(times) / len(times)
+        threads = min(16, os.cpu_count() or 1)
+        want_leaves, want = orc.root_synthetic(total, size, SEED, nthreads=threads, want_leaves=True)
+        parity = {"root": root.hex(), "cpu_root": want.hex(),
+                  "bit_exact": root == want and b"".join(leaves) == want_leaves}
+        if nfiles == 256 and size == 32 << 20:
+            parity["fixture_root"] = golden_case("config1_8192MiB_chunk32MiB")["root"]
+            parity["bit_exact"] = parity["bit_exact"] and root.hex() == parity["fixture_root"]
+        out = {
+            "metric": "GiB/s of files hashed to a Merkle root through NewHashTree(chunkPath) (page cache -> root)",
+            "value": round(total / tavg / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(tavg * 1e3, 3), "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": "u32",
+            "data": f"synthetic: {nfiles} files in {'/dev/shm' if base else 'the temp dir'} (page cache)",
+            "config": {"workload": f"{nfiles} files x {size} B ({total} B), one leaf per file",
+                       "files": nfiles, "file_bytes": size, "leaf_kernel": ctx.leaf_kernel_for(nfiles)},
+            "step_ms": [round(t * 1e3, 2) for t in times],
+            "parity": parity,
+        }
+        if not args.no_cpu:
+            # faithful serial restatement of types.go:24-38 on a sample: read each file whole, then hash
+            sample = paths[:min(nfiles, 16)]
+            t0 = time.perf_counter()
+            chunks = []
+            for p in sample:
+                with open(p, "rb") as f:
+                    chunks.append(f.read())
+            orc.root_chunks(chunks, nthreads=1)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": round(len(sample) * size / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
+                                   "kind": "port", "sample": f"{len(sample)} of the same files: read whole (io.ReadAll), "
+                                   "then serial SHA-256 leaves + tree (oracle/merkle_oracle.c, SHA-NI)"}
+            del chunks
+        print(json.dumps(out), flush=True)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def run_plumbing(args, torch, dist, world, rank, device, dev_index, gloo):
+    """BASELINE configs[0]: one 64 MiB synthetic object at 32 MiB chunks (2 leaves) -- the
+    reference's CPU plumbing config.  Times the faithful serial CPU restatement (the stand-in for
+    the Go path) and the GPU path on the same bytes; both roots against the committed fixture."""
+    from deoss_amd import MerkleContext
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    case = golden_case("config0_64MiB_chunk32MiB")
+    length, chunk, seed = case["len"], case["chunk"], case["seed"]
+    orc = Oracle()
+    host = torch.empty(length, dtype=torch.uint8)
+    orc.fill_splitmix_ptr(host.data_ptr(), 0, length, seed)
+    reps = max(args.steps, 3)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _, cpu_root = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=1)
+    cpu_s = (time.perf_counter() - t0) / reps
+    ctx = MerkleContext(devices=[dev_index])
+    buf = torch.empty(length + 64, dtype=torch.uint8, device=device)
+    sptr = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, length, seed, sptr)
+    root_dev = torch.zeros(32, dtype=torch.uint8, device=device)
+    elapsed, n, k_sum, _ = timed_steps(args, torch, dist, world, device, gloo, ctx,
+                                       lambda: ctx.root_device_async(buf.data_ptr(), length, chunk,
+                                                                     root_dev.data_ptr(), 0, sptr))
+    gpu_root = bytes(root_dev.cpu().numpy()).hex()
+    out = {
+        "metric": "BASELINE configs[0]: 64 MiB object through common/hashtree (CPU plumbing config)",
+        "value": round(length / cpu_s / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 0, "steps": reps,
+        "warmup": 0, "ms_per_step": round(cpu_s * 1e3, 3), "higher_is_better": True, "scaling": "none",
+        "vs_baseline": None, "dtype": "u32", "data": "synthetic splitmix64 object (seed 0xDE0550000)",
+        "config": {"workload": f"configs[0]: 1 object of {length} B, chunk {chunk} B (2 leaves)", "object_bytes": length,
+                   "chunk": chunk},
+        "cpu": {"kind": "port", "cores": 1, "seconds": round(cpu_s, 4),
+                "what": "oracle/merkle_oracle.c faithful serial restatement (SHA-NI), stands in for Go common/hashtree"},
+        "gpu": {"device_resident_GiBps": round(length * args.steps / elapsed / (1 << 30), 4),
+                "ms_per_root": round(elapsed / args.steps * 1e3, 3), "leaf_kernel": ctx.leaf_kernel_for(2)},
+        "parity": {"fixture_root": case["root"], "cpu_root": cpu_root.hex(), "gpu_root": gpu_root,
+                   "bit_exact": cpu_root.hex() == case["root"] == gpu_root},
+    }
+    print(json.dumps(out), flush=True)
 
 
 def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):

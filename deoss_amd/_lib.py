@@ -26,7 +26,7 @@ DM_ERR_NODEV = -7
 
 # Every symbol include/deoss_merkle.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
-    "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count",
+    "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count", "dm_gpu_count",
     "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
     "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
     "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_set_leaf_kernel", "dm_leaf_kernel_for",
@@ -63,6 +63,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_strerror": ([i32], ctypes.c_char_p),
         "dm_last_error": ([vp], ctypes.c_char_p),
         "dm_device_count": ([vp], i32),
+        "dm_gpu_count": ([], i32),
         "dm_new_hash_tree": ([vp, ctypes.POINTER(ctypes.c_char_p), u64, vp, vp], i32),
         "dm_root_chunks": ([vp, pvp, pu64, u64, vp, vp], i32),
         "dm_root_buffer": ([vp, vp, u64, u64, vp, vp], i32),

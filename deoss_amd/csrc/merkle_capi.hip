@@ -19,6 +19,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -124,6 +125,18 @@ struct dm_ctx {
 
 namespace {
 
+// Detailed message of the calling thread's last failing call (dm_last_error).  Thread-local, so a
+// reader never races another thread's failure (Go: runtime.LockOSThread around call + read), and
+// every error return below sets it, so it is never a stale message from an older call.
+thread_local std::string t_err;
+
+int set_err(int code, const char* msg) {
+    t_err = msg;
+    return code;
+}
+
+int bad_arg() { return set_err(DM_ERR_INVALID, "invalid argument"); }
+
 int fail(dm_ctx* c, int code, const char* fmt, ...) {
     char buf[1024];
     va_list ap;
@@ -131,6 +144,7 @@ int fail(dm_ctx* c, int code, const char* fmt, ...) {
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
     if (c) c->err = buf;
+    t_err = buf;
     return code;
 }
 
@@ -636,12 +650,17 @@ int reduce_leaves_to_host(dm_ctx* c, Dev& d, uint64_t n, uint8_t* leaf_out, uint
     return DM_OK;
 }
 
-// Multi-device single object from host memory: aligned leaf ranges per device, subtree roots,
-// RCCL all-gather, final levels on device 0.
-int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out,
-                      uint8_t root[32]) {
+// Leaf producer of the multi-device path: fills d.leaves with the digests of leaves [l0, l1)
+// (stream-ordered on d.stream), reporting errors into its own context `cc`.
+using LeafProducer = std::function<int(dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1)>;
+
+// Multi-device single object: aligned leaf ranges per device (blocks of 2^k leaves, round-robin
+// free contiguous ranges), each device's leaf digests from ONE pass of `produce` (they feed both
+// the k-level subtree reduce and leaf_out), one RCCL all-gather of the 32-byte level-k nodes,
+// final levels on device 0.  Odd-node duplication only ever touches the global last node, which
+// lives in the last block, so the per-device nodes are exactly the global level-k nodes.
+int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf_out, uint8_t root[32]) {
     const int G = (int)c->devs.size();
-    const uint64_t n = ceil_div(len, chunk);
     // block = 2^k leaves with at least 2 blocks per device when possible
     uint32_t k = 0;
     while (ceil_shift(n, k + 1) >= (uint64_t)(2 * G)) k++;
@@ -654,9 +673,10 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
         cnt[g] = b_hi[g] - b_lo[g];
         maxc = std::max(maxc, cnt[g]);
     }
+    // order this call's scratch use after every call still queued on another stream of each device
+    for (int g = 0; g < G; g++) RC_TRY(begin_call(c, c->devs[g], c->devs[g].stream));
     std::vector<int> rcs(G, DM_OK);
     std::vector<std::string> errs(G);
-    // per-device: H2D of its byte range + subtree to k levels (parallel host threads)
     auto work = [&](int g) {
         Dev& d = c->devs[g];
         dm_ctx local;   // private error sink (no devices: helpers given it must not index devs)
@@ -664,36 +684,27 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
         dm_ctx* cc = &local;
         int rc = DM_OK;
         do {
-            if (hipSetDevice(d.id) != hipSuccess) { rc = DM_ERR_HIP; break; }
+            if (hipSetDevice(d.id) != hipSuccess) { rc = fail(cc, DM_ERR_HIP, "hipSetDevice(%d)", d.id); break; }
             const uint64_t l0 = b_lo[g] * S, l1 = std::min(n, b_hi[g] * S);
+            if (d.gather.ensure(std::max<uint64_t>(maxc, 1) * 32 * (G + 1)) != hipSuccess) {
+                rc = fail(cc, DM_ERR_NOMEM, "gather slots");
+                break;
+            }
             if (l1 <= l0) break;
-            const uint64_t byte0 = l0 * chunk, byte1 = std::min(len, l1 * chunk);
-            if (d.data.ensure(byte1 - byte0) != hipSuccess || d.gather.ensure(std::max<uint64_t>(maxc, 1) * 32 * (G + 1)) != hipSuccess) {
-                rc = DM_ERR_NOMEM;
-                break;
-            }
-            if (hipMemcpy(d.data.p, static_cast<const uint8_t*>(host) + byte0, byte1 - byte0, hipMemcpyHostToDevice) != hipSuccess) {
-                rc = DM_ERR_HIP;
-                break;
-            }
-            dm::LeafArgs la = uniform_args(d.data.p, byte1 - byte0, chunk);
-            uint64_t nout = 0;
-            if (leaf_out) {
-                if (d.leaves.ensure((l1 - l0) * 32 + 256) != hipSuccess) { rc = DM_ERR_NOMEM; break; }
-            }
-            // leaf digests for leaf_out are produced by a separate K1 pass only when requested
-            rc = run_tree(cc, d, d.stream, la, false, (chunk % 16) == 0, (int)k, d.gather.u8(), &nout,
-                          nullptr);
-            if (rc != DM_OK) break;
-            if (leaf_out) {
-                dm::LeafArgs lb = uniform_args(d.data.p, byte1 - byte0, chunk);
-                uint64_t n2 = 0;
-                rc = run_tree(cc, d, d.stream, lb, false, (chunk % 16) == 0, 0, d.leaves.u8(), &n2, nullptr);
-                if (rc != DM_OK) break;
-                if (hipMemcpyAsync(leaf_out + 32 * l0, d.leaves.p, (l1 - l0) * 32, hipMemcpyDeviceToHost, d.stream) != hipSuccess) {
-                    rc = DM_ERR_HIP;
+            const uint64_t nl = l1 - l0;
+            if ((rc = produce(cc, d, l0, l1)) != DM_OK) break;
+            // exactly k levels of this device's blocks (odd levels self-pair inside the last block)
+            if (k == 0) {
+                if (hipMemcpyAsync(d.gather.p, d.leaves.p, nl * 32, hipMemcpyDeviceToDevice, d.stream) != hipSuccess) {
+                    rc = fail(cc, DM_ERR_HIP, "level-0 copy");
                     break;
                 }
+            } else if ((rc = reduce_stages(cc, d, d.stream, d.leaves.u8(), nl, k, d.gather.u8())) != DM_OK) {
+                break;
+            }
+            if (leaf_out && hipMemcpyAsync(leaf_out + 32 * l0, d.leaves.p, nl * 32, hipMemcpyDeviceToHost, d.stream) != hipSuccess) {
+                rc = fail(cc, DM_ERR_HIP, "leaf digests D2H");
+                break;
             }
         } while (0);
         rcs[g] = rc;
@@ -705,7 +716,11 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
         for (auto& t : th) t.join();
     }
     for (int g = 0; g < G; g++)
-        if (rcs[g] != DM_OK) return fail(c, rcs[g], "device %d: %s", c->devs[g].id, errs[g].c_str());
+        if (rcs[g] != DM_OK) {
+            // a file error keeps the Go message shape ("open <path>: ..."): no device prefix
+            if (rcs[g] == DM_ERR_IO || rcs[g] == DM_ERR_EMPTY) return fail(c, rcs[g], "%s", errs[g].c_str());
+            return fail(c, rcs[g], "device %d: %s", c->devs[g].id, errs[g].c_str());
+        }
     // C1: all-gather of fixed-size slots (maxc nodes of 32 B per device) over RCCL
     const size_t slot = maxc * 32;
     NCCL_TRY(ncclGroupStart());
@@ -716,18 +731,17 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
     NCCL_TRY(ncclGroupEnd());
     Dev& d0 = c->devs[0];
     HIP_TRY(hipSetDevice(d0.id));
-    // compact the gathered slots into block order on device 0
+    // compact the gathered slots into block order on device 0, in d0.leaves (K2's scratch is
+    // nodes_a/b) once device 0's leaf_out copy has left it
+    HIP_TRY(hipStreamSynchronize(d0.stream));
+    HIP_TRY(d0.leaves.ensure(std::max<uint64_t>(nb, 1) * 32 + 256));
     uint64_t total = 0;
-    HIP_TRY(d0.nodes_b.ensure(nb * 32 + 256));
     for (int g = 0; g < G; g++) {
         if (cnt[g] == 0) continue;
-        HIP_TRY(hipMemcpyAsync(d0.nodes_b.u8() + 32 * total, d0.gather.u8() + slot + g * slot, cnt[g] * 32,
+        HIP_TRY(hipMemcpyAsync(d0.leaves.u8() + 32 * total, d0.gather.u8() + slot + g * slot, cnt[g] * 32,
                                hipMemcpyDeviceToDevice, d0.stream));
         total += cnt[g];
     }
-    // nodes_b is also K2 scratch: move the block roots to `leaves` first
-    HIP_TRY(d0.leaves.ensure(std::max<uint64_t>(nb * 32, n * 32) + 256));
-    HIP_TRY(hipMemcpyAsync(d0.leaves.p, d0.nodes_b.p, nb * 32, hipMemcpyDeviceToDevice, d0.stream));
     RC_TRY(finish(c, d0, d0.stream, d0.leaves.u8(), nb, k == 0, d0.root.u8()));
     HIP_TRY(hipMemcpyAsync(root, d0.root.p, 32, hipMemcpyDeviceToHost, d0.stream));
     for (int g = 0; g < G; g++) {
@@ -735,6 +749,19 @@ int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk,
         HIP_TRY(hipStreamSynchronize(c->devs[g].stream));
     }
     return DM_OK;
+}
+
+// Multi-device host buffer: each device stages its byte range through its own pinned ring (or
+// straight from pinned memory) with H2D overlapped with leaf hashing (h2d_and_hash_leaves:
+// stripes for few long leaves).
+int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out,
+                      uint8_t root[32]) {
+    const uint64_t n = ceil_div(len, chunk);
+    auto produce = [&](dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1) -> int {
+        const uint64_t byte0 = l0 * chunk, byte1 = std::min(len, l1 * chunk);
+        return h2d_and_hash_leaves(cc, d, static_cast<const uint8_t*>(host) + byte0, byte1 - byte0, chunk);
+    };
+    return multi_root(c, n, produce, leaf_out, root);
 }
 
 }  // namespace
@@ -756,22 +783,31 @@ const char* dm_strerror(int rc) {
     }
 }
 
-const char* dm_last_error(dm_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+const char* dm_last_error(dm_ctx*) { return t_err.c_str(); }
 
 int dm_device_count(dm_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
 
+int dm_gpu_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
 int dm_create(dm_ctx** out, const int* devs, int ndev) {
-    if (!out) return DM_ERR_INVALID;
+    if (!out) return bad_arg();
     *out = nullptr;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return DM_ERR_NODEV;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return set_err(DM_ERR_NODEV, "no usable GPU");
     std::vector<int> ids;
     if (!devs || ndev <= 0) ids.push_back(0);
     else ids.assign(devs, devs + ndev);
     for (size_t i = 0; i < ids.size(); i++) {
-        if (ids[i] < 0 || ids[i] >= count) return DM_ERR_INVALID;
+        if (ids[i] < 0 || ids[i] >= count) return bad_arg();
         for (size_t j = 0; j < i; j++)
-            if (ids[j] == ids[i]) return DM_ERR_INVALID;
+            if (ids[j] == ids[i]) return bad_arg();
     }
     dm_ctx* c = new dm_ctx();
     c->devs.resize(ids.size());
@@ -790,7 +826,7 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
         if (ncclCommInitAll(c->comms.data(), (int)ids.size(), ids.data()) != ncclSuccess) {
             c->comms.clear();
             dm_destroy(c);
-            return DM_ERR_RCCL;
+            return set_err(DM_ERR_RCCL, "ncclCommInitAll failed");
         }
     }
     *out = c;
@@ -805,20 +841,20 @@ void dm_destroy(dm_ctx* ctx) {
 }
 
 int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
-    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_QUAD) return DM_ERR_INVALID;
+    if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_QUAD) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->leaf_mode = mode;
     return DM_OK;
 }
 
 int dm_leaf_kernel_for(dm_ctx* ctx, uint64_t nleaves) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     return pick_leaf_kernel(ctx, ctx->devs[0], nleaves);
 }
 
 int dm_set_timing(dm_ctx* ctx, int enable) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     ctx->timing = enable != 0;
     for (auto& d : ctx->devs) d.ntimed = 0;
@@ -826,7 +862,7 @@ int dm_set_timing(dm_ctx* ctx, int enable) {
 }
 
 int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double* total_ms_sum, double* leaf_ms_max) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     uint64_t n = 0;
@@ -854,7 +890,7 @@ int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double
 
 int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, void* dev_root,
                          void* leaf_out_dev, void* stream) {
-    if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return DM_ERR_INVALID;
+    if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     Dev& d = ctx->devs[0];
     return root_device_impl(ctx, d, pick_stream(d, stream), dev, len, chunk, static_cast<uint8_t*>(dev_root),
@@ -862,7 +898,7 @@ int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t ch
 }
 
 int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint8_t root[32]) {
-    if (!ctx || !root || chunk == 0 || (!dev && len)) return DM_ERR_INVALID;
+    if (!ctx || !root || chunk == 0 || (!dev && len)) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     Dev& d = c->devs[0];
@@ -874,7 +910,7 @@ int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, u
 
 int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint32_t levels,
                             void* dev_nodes, uint64_t* n_out, void* stream) {
-    if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return DM_ERR_INVALID;
+    if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -891,7 +927,7 @@ int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t
 
 int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int min_one_level, void* dev_root,
                            void* stream) {
-    if (!ctx || !dev_nodes || !dev_root) return DM_ERR_INVALID;
+    if (!ctx || !dev_nodes || !dev_root) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -904,7 +940,7 @@ int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int m
 
 int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const uint64_t* lens, uint64_t nobj,
                                uint64_t chunk, void* dev_roots, void* stream) {
-    if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return DM_ERR_INVALID;
+    if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
@@ -915,7 +951,7 @@ int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const u
 }
 
 int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbytes, uint64_t seed, void* stream) {
-    if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return DM_ERR_INVALID;
+    if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nbytes == 0) return DM_OK;
@@ -931,7 +967,7 @@ int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbyte
 }
 
 int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32]) {
-    if (!ctx || !root || chunk == 0 || (!host && len)) return DM_ERR_INVALID;
+    if (!ctx || !root || chunk == 0 || (!host && len)) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -945,7 +981,7 @@ int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, 
 
 int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out,
                    uint8_t root[32]) {
-    if (!ctx || !root || (n && (!ptrs || !lens))) return DM_ERR_INVALID;
+    if (!ctx || !root || (n && (!ptrs || !lens))) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -971,7 +1007,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
 
 int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
                   uint8_t* roots) {
-    if (!ctx || chunk == 0 || (nobj && (!objs || !lens || !roots))) return DM_ERR_INVALID;
+    if (!ctx || chunk == 0 || (nobj && (!objs || !lens || !roots))) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
@@ -990,46 +1026,11 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
     return DM_OK;
 }
 
-int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t* leaf_out, uint8_t root[32]) {
-    if (!ctx || !root || (n && !paths)) return DM_ERR_INVALID;
-    dm_ctx* c = ctx;
-    if (n == 0) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        return fail(c, DM_ERR_EMPTY, "Empty data");
-    }
-    // types.go:24-35: open and read every file whole, in order; the first error is returned.
-    std::vector<std::vector<uint8_t>> bufs(n);
-    for (uint64_t i = 0; i < n; i++) {
-        FILE* f = paths[i] ? std::fopen(paths[i], "rb") : nullptr;
-        if (!f) {
-            std::string m = std::strerror(errno);
-            if (!m.empty()) m[0] = (char)std::tolower((unsigned char)m[0]);
-            std::lock_guard<std::mutex> lk(ctx->mu);
-            return fail(c, DM_ERR_IO, "open %s: %s", paths[i] ? paths[i] : "(null)", m.c_str());
-        }
-        uint8_t tmp[1 << 16];
-        size_t r;
-        while ((r = std::fread(tmp, 1, sizeof tmp, f)) > 0) bufs[i].insert(bufs[i].end(), tmp, tmp + r);
-        const bool bad = std::ferror(f) != 0;
-        std::fclose(f);
-        if (bad) {
-            std::lock_guard<std::mutex> lk(ctx->mu);
-            return fail(c, DM_ERR_IO, "read %s: i/o error", paths[i]);
-        }
-    }
-    std::vector<const void*> ptrs(n);
-    std::vector<uint64_t> lens(n);
-    for (uint64_t i = 0; i < n; i++) {
-        ptrs[i] = bufs[i].data();
-        lens[i] = bufs[i].size();
-    }
-    return dm_root_chunks(ctx, ptrs.data(), lens.data(), n, leaf_out, root);
-}
-
 }  // extern "C"
 
 // Streaming (incremental) roots: dm_stream_* (shares the helpers above).
 #include "merkle_stream.inl"
+#include "files_capi.inl"
 #include "rs_capi.inl"
 #include "process_capi.inl"
 #include "tree_capi.inl"

@@ -61,6 +61,7 @@ int sfail(dm_stream* st, int code, const char* what, hipError_t e) {
     char buf[512];
     snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
     st->err = buf;
+    t_err = buf;
     return code;
 }
 
@@ -185,7 +186,7 @@ void stream_free(dm_stream* st) {
 extern "C" {
 
 int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
-    if (!ctx || !out || chunk == 0) return DM_ERR_INVALID;
+    if (!ctx || !out || chunk == 0) return bad_arg();
     *out = nullptr;
     if (chunk % 16 != 0) {
         std::lock_guard<std::mutex> lk(ctx->mu);
@@ -224,6 +225,7 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     if (rc != DM_OK) {
         std::lock_guard<std::mutex> lk(ctx->mu);
         ctx->err = st->err;
+        t_err = st->err;
         stream_free(st);
         return rc;
     }
@@ -232,7 +234,7 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
 }
 
 int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
-    if (!st || (!data && len)) return DM_ERR_INVALID;
+    if (!st || (!data && len)) return bad_arg();
     SHIP(hipSetDevice(st->c->devs[st->dev].id));
     const uint8_t* p = static_cast<const uint8_t*>(data);
     while (len) {
@@ -257,9 +259,10 @@ int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
 const char* dm_stream_error(dm_stream* st) { return st ? st->err.c_str() : ""; }
 
 int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_t* nleaves, uint8_t root[32]) {
-    if (!st || !root) return DM_ERR_INVALID;
+    if (!st || !root) return bad_arg();
     dm_ctx* c = st->c;
     int rc = DM_OK;
+    t_err.clear();
     do {
         if (st->received == 0) {
             rc = DM_ERR_EMPTY;
@@ -302,6 +305,7 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
     if (rc != DM_OK && !st->err.empty()) {
         std::lock_guard<std::mutex> lk(c->mu);
         if (c->err.empty() || rc == DM_ERR_EMPTY) c->err = st->err;
+        if (t_err.empty() || rc == DM_ERR_EMPTY) t_err = st->err;
     }
     stream_free(st);
     return rc;

@@ -147,7 +147,7 @@ extern "C" {
 
 int dm_process_device_async(dm_rs* r, void* dev_obj, uint64_t len, uint64_t segment, void* dev_parity,
                             void* dev_seg_hashes, void* dev_frag_hashes, void* dev_fid, void* stream) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     RC_TRY(process_check(r, len, segment));
@@ -161,7 +161,7 @@ int dm_process_device_async(dm_rs* r, void* dev_obj, uint64_t len, uint64_t segm
 
 int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment, void* frags_out,
                       uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t fid[32]) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!fid || (!host && len)) return fail(c, DM_ERR_INVALID, "dm_process_buffer: null argument");
@@ -171,7 +171,7 @@ int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment
 
 int dm_process_batch(dm_rs* r, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t segment,
                      void* const* frags_out, uint8_t* const* seg_hashes, uint8_t* const* frag_hashes, uint8_t* fids) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     if (nobj == 0) return DM_OK;

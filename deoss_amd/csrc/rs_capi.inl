@@ -171,7 +171,7 @@ int rs_reconstruct_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* const* shards, 
 extern "C" {
 
 int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
-    if (!ctx || !out) return DM_ERR_INVALID;
+    if (!ctx || !out) return bad_arg();
     *out = nullptr;
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
@@ -229,14 +229,14 @@ void dm_rs_destroy(dm_rs* r) {
 }
 
 int dm_rs_matrix(dm_rs* r, uint8_t* out) {
-    if (!r || !out) return DM_ERR_INVALID;
+    if (!r || !out) return bad_arg();
     std::memcpy(out, r->mat.data(), r->mat.size());
     return DM_OK;
 }
 
 int dm_rs_encode_device_async(dm_rs* r, const void* data, uint64_t data_stride, void* parity, uint64_t parity_stride,
                               uint64_t shard, uint64_t nseg, void* stream) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!data || !parity || nseg == 0 || shard == 0 || shard % 16 || data_stride % 16 || parity_stride % 16 ||
@@ -267,7 +267,7 @@ int dm_rs_encode_device_async(dm_rs* r, const void* data, uint64_t data_stride, 
 
 int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t* present, uint64_t shard,
                                    void* stream) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!shards || !present || shard == 0 || shard % 16)
@@ -284,7 +284,7 @@ int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t*
 // Host shards: staged in one device buffer at a 16-byte pitch (padding positions are coded too
 // and never copied back; positions are independent).
 int dm_rs_encode(dm_rs* r, const void* const* data, void* const* parity, uint64_t shard) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     if (!data || !parity || shard == 0) return fail(c, DM_ERR_INVALID, "dm_rs_encode: null shards or zero size");
@@ -317,7 +317,7 @@ int dm_rs_encode(dm_rs* r, const void* const* data, void* const* parity, uint64_
 }
 
 int dm_rs_encode_buffer(dm_rs* r, const void* host, uint64_t len, void* out, uint64_t* per_shard) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     if (!per_shard || !out || (!host && len)) return fail(r->c, DM_ERR_INVALID, "dm_rs_encode_buffer: null argument");
     if (len == 0) return fail(r->c, DM_ERR_EMPTY, "Empty data");   // klauspost ErrShortData
     const uint64_t per = ceil_div(len, (uint64_t)r->k);
@@ -334,7 +334,7 @@ int dm_rs_encode_buffer(dm_rs* r, const void* host, uint64_t len, void* out, uin
 }
 
 int dm_rs_reconstruct(dm_rs* r, void* const* shards, const uint8_t* present, uint64_t shard) {
-    if (!r) return DM_ERR_INVALID;
+    if (!r) return bad_arg();
     dm_ctx* c = r->c;
     std::lock_guard<std::mutex> lk(c->mu);
     const int total = r->k + r->m;
@@ -363,7 +363,7 @@ int dm_rs_reconstruct(dm_rs* r, void* const* shards, const uint8_t* present, uin
 }
 
 int dm_rs_verify(dm_rs* r, const void* const* shards, uint64_t shard, int* ok) {
-    if (!r || !ok) return DM_ERR_INVALID;
+    if (!r || !ok) return bad_arg();
     *ok = 0;
     if (!shards || shard == 0) return fail(r->c, DM_ERR_INVALID, "dm_rs_verify: bad arguments");
     std::vector<std::vector<uint8_t>> mine(r->m, std::vector<uint8_t>(shard));

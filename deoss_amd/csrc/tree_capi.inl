@@ -115,7 +115,7 @@ uint64_t dm_tree_node_count(uint64_t n) { return tree_nodes(n); }
 uint32_t dm_tree_depth(uint64_t n) { return tree_depth(n); }
 
 int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n, void* dev_nodes, void* stream) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -128,7 +128,7 @@ int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n,
 }
 
 int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t* nodes_out) {
-    if (!ctx || (n && (!leaf_digests || !nodes_out))) return DM_ERR_INVALID;
+    if (!ctx || (n && (!leaf_digests || !nodes_out))) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -147,7 +147,7 @@ int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t
 
 int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void* dev_nodes, uint64_t n,
                                  const void* dev_idx, uint64_t q, void* dev_paths, void* dev_bits, void* stream) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -165,7 +165,7 @@ int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void
 
 int dm_merkle_paths(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, const uint64_t* idx, uint64_t q,
                     uint8_t* paths, uint8_t* bits) {
-    if (!ctx || (n && !leaf_digests) || (q && (!idx || !paths || !bits))) return DM_ERR_INVALID;
+    if (!ctx || (n && !leaf_digests) || (q && (!idx || !paths || !bits))) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -194,7 +194,7 @@ int dm_merkle_paths(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, const 
 int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, const uint64_t* lens, uint64_t q,
                                  const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                  uint64_t root_stride, void* dev_ok, void* stream) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
@@ -215,7 +215,7 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
 int dm_verify_object_device_async(dm_ctx* ctx, const void* dev_obj, uint64_t len, uint64_t chunk,
                                   const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                   uint64_t root_stride, void* dev_ok, void* stream) {
-    if (!ctx) return DM_ERR_INVALID;
+    if (!ctx) return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
@@ -234,7 +234,7 @@ int dm_verify_paths(dm_ctx* ctx, const void* const* contents, const uint64_t* le
                     const uint8_t* bits, uint32_t depth, const uint8_t* roots, uint64_t root_stride, uint8_t* ok) {
     if (!ctx || (q && (!contents || !lens || !paths || !bits || !roots || !ok)) || depth == 0 ||
         (root_stride != 0 && root_stride != 32))
-        return DM_ERR_INVALID;
+        return bad_arg();
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;

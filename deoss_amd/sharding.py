@@ -65,6 +65,18 @@ def plan_shards(length: int, chunk: int, world: int) -> ShardPlan:
     return ShardPlan(length=length, chunk=chunk, world=world, k=best, n_leaves=n, n_blocks=nb)
 
 
+def parity_prefix(length: int, chunk: int, cap_bytes: int) -> int:
+    """Bytes of the prefix the multi-GPU parity leg re-roots on one GPU: the whole object when it
+    fits in cap_bytes, else the largest whole-chunk prefix that does (bench.py multi_rank_parity;
+    SURVEY.md 8d config 4: "vs the single-GPU root on a <= 64 GiB prefix")."""
+    if length <= cap_bytes:
+        return length
+    p = cap_bytes // chunk * chunk
+    if p <= 0:
+        raise ValueError("prefix cap smaller than one chunk")
+    return p
+
+
 def sharded_root(plan: ShardPlan, rank: int, local_subtree: Callable[[int], "object"],
                  finish: Callable[["object", int, bool], "object"], torch_mod, dist_mod,
                  device, group=None, comm_device=None):

@@ -40,3 +40,46 @@ func TestNewHashTreeGPU(t *testing.T) {
 	_, err = NewHashTree(nil)
 	assert.EqualError(t, err, "Empty data")
 }
+
+// NewHashTreeFromBuffer rejects a non-positive chunk size with an error (no panic).
+func TestFromBufferChunkSize(t *testing.T) {
+	_, err := NewHashTreeFromBuffer([]byte("abc"), 0)
+	assert.Error(t, err)
+	_, err = NewHashTreeFromBuffer([]byte("abc"), -5)
+	assert.Error(t, err)
+}
+
+// A Stream fed in uneven pieces builds the same tree as NewHashTreeFromBuffer over the whole body.
+func TestStreamGPU(t *testing.T) {
+	body := make([]byte, 9<<20+123)
+	for i := range body {
+		body[i] = byte(i*131 + i>>9)
+	}
+	want, err := NewHashTreeFromBuffer(body, 1<<20)
+	assert.NoError(t, err)
+	hs, err := NewStream(1 << 20)
+	assert.NoError(t, err)
+	for pos, step := 0, 1; pos < len(body); step = step*7%1000003 + 1 {
+		n := min(step, len(body)-pos)
+		w, err := hs.Write(body[pos : pos+n])
+		assert.NoError(t, err)
+		assert.Equal(t, n, w)
+		pos += n
+	}
+	got, err := hs.Close()
+	assert.NoError(t, err)
+	assert.Equal(t, want.MerkleRoot(), got.MerkleRoot())
+	assert.Equal(t, len(want.Leafs), len(got.Leafs))
+
+	empty, err := NewStream(1 << 20)
+	assert.NoError(t, err)
+	_, err = empty.Close()
+	assert.EqualError(t, err, "Empty data")
+
+	aborted, err := NewStream(64)
+	assert.NoError(t, err)
+	_, _ = aborted.Write(body[:1000])
+	aborted.Abort()
+	_, err = aborted.Close()
+	assert.Error(t, err)
+}

@@ -17,6 +17,7 @@ import "C"
 
 import (
 	"errors"
+	"runtime"
 	"unsafe"
 
 	"github.com/cbergoon/merkletree"
@@ -49,6 +50,8 @@ func GetMerklePaths(t *merkletree.MerkleTree, leaves []int) ([][][]byte, [][]int
 	q := uint64(len(leaves))
 	paths := make([]byte, 32*depth*q)
 	bits := make([]byte, depth*q)
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	rc := C.dm_merkle_paths(c, (*C.uint8_t)(unsafe.Pointer(&digests[0])), C.uint64_t(n),
 		(*C.uint64_t)(unsafe.Pointer(&idx[0])), C.uint64_t(q), (*C.uint8_t)(unsafe.Pointer(&paths[0])),
 		(*C.uint8_t)(unsafe.Pointer(&bits[0])))
@@ -107,6 +110,8 @@ func VerifyProofs(contents [][]byte, paths [][][]byte, index [][]int64, root []b
 		}
 	}
 	ok := make([]byte, q)
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	rc := C.dm_verify_paths(c, (*unsafe.Pointer)(ptrs), (*C.uint64_t)(unsafe.Pointer(&lens[0])), C.uint64_t(q),
 		(*C.uint8_t)(unsafe.Pointer(&pb[0])), (*C.uint8_t)(unsafe.Pointer(&bb[0])), C.uint32_t(depth),
 		(*C.uint8_t)(unsafe.Pointer(&root[0])), 0, (*C.uint8_t)(unsafe.Pointer(&ok[0])))

@@ -2,7 +2,9 @@
 
 // Drop-in replacement for DeOSS common/hashtree/types.go (reference lines 19-39): the same
 // NewHashTree signature and errors, with leaf hashing and the root on the GPU through the
-// C ABI in include/deoss_merkle.h.
+// C ABI in include/deoss_merkle.h.  One process-wide context spans every GPU chosen by Init or
+// DEOSS_GPUS (default: all visible GPUs), so a large object or file list shards by aligned chunk
+// ranges across the node's GPUs with one RCCL all-gather of subtree roots.
 package hashtree
 
 /*
@@ -17,6 +19,10 @@ import (
 	"bytes"
 	"errors"
 	"fmt"
+	"os"
+	"runtime"
+	"strconv"
+	"strings"
 	"sync"
 	"unsafe"
 
@@ -24,20 +30,79 @@ import (
 )
 
 var (
-	ctxOnce sync.Once
-	ctx     *C.dm_ctx
-	ctxErr  error
+	ctxMu  sync.Mutex
+	ctx    *C.dm_ctx
+	ctxErr error
+	devSel []int // nil: DEOSS_GPUS, else every visible GPU
 )
 
-func gpu() (*C.dm_ctx, error) {
-	ctxOnce.Do(func() {
-		if rc := C.dm_create(&ctx, nil, 0); rc != C.DM_OK {
-			ctxErr = errors.New(C.GoString(C.dm_strerror(rc)))
+// Init selects the GPUs (HIP device ids) the package's context spans.  It must run before the
+// first NewHashTree / NewHashTreeFromBuffer / NewStream call; later calls return an error.
+// Without Init the context uses DEOSS_GPUS ("0,1,2,3" or "all"), else every visible GPU.
+func Init(devs []int) error {
+	ctxMu.Lock()
+	defer ctxMu.Unlock()
+	if ctx != nil || ctxErr != nil {
+		return errors.New("hashtree: Init after first use")
+	}
+	if len(devs) == 0 {
+		return errors.New("hashtree: Init needs at least one device")
+	}
+	devSel = append([]int(nil), devs...)
+	return nil
+}
+
+func deviceList() ([]int, error) {
+	if devSel != nil {
+		return devSel, nil
+	}
+	spec := strings.TrimSpace(os.Getenv("DEOSS_GPUS"))
+	if spec != "" && spec != "all" {
+		var out []int
+		for _, f := range strings.Split(spec, ",") {
+			d, err := strconv.Atoi(strings.TrimSpace(f))
+			if err != nil || d < 0 {
+				return nil, fmt.Errorf("hashtree: bad DEOSS_GPUS entry %q", f)
+			}
+			out = append(out, d)
 		}
-	})
+		return out, nil
+	}
+	n := int(C.dm_gpu_count())
+	if n <= 0 {
+		return nil, errors.New(C.GoString(C.dm_strerror(C.DM_ERR_NODEV)))
+	}
+	out := make([]int, n)
+	for i := range out {
+		out[i] = i
+	}
+	return out, nil
+}
+
+func gpu() (*C.dm_ctx, error) {
+	ctxMu.Lock()
+	defer ctxMu.Unlock()
+	if ctx != nil || ctxErr != nil {
+		return ctx, ctxErr
+	}
+	devs, err := deviceList()
+	if err != nil {
+		ctxErr = err
+		return nil, err
+	}
+	cdevs := make([]C.int, len(devs))
+	for i, d := range devs {
+		cdevs[i] = C.int(d)
+	}
+	if rc := C.dm_create(&ctx, &cdevs[0], C.int(len(cdevs))); rc != C.DM_OK {
+		ctx = nil
+		ctxErr = errors.New(C.GoString(C.dm_strerror(rc)))
+	}
 	return ctx, ctxErr
 }
 
+// rcError reads the library's thread-local message of the failing call: the caller holds
+// runtime.LockOSThread from the call until here.
 func rcError(c *C.dm_ctx, rc C.int) error {
 	if rc == C.DM_ERR_EMPTY {
 		return errors.New("Empty data") // types.go:21
@@ -87,6 +152,8 @@ func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error) {
 	}()
 	leaves := make([]byte, 32*len(chunkPath))
 	root := make([]byte, 32)
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
 	rc := C.dm_new_hash_tree(c, (**C.char)(unsafe.Pointer(&cpaths[0])), C.uint64_t(len(chunkPath)),
 		(*C.uint8_t)(unsafe.Pointer(&leaves[0])), (*C.uint8_t)(unsafe.Pointer(&root[0])))
 	if rc != C.DM_OK {
@@ -98,6 +165,9 @@ func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error) {
 // NewHashTreeFromBuffer (additive): the upload body already in memory, split into chunkSize
 // chunks (the last one short) -- no temp files, one H2D pass.
 func NewHashTreeFromBuffer(buf []byte, chunkSize int) (*merkletree.MerkleTree, error) {
+	if chunkSize <= 0 {
+		return nil, fmt.Errorf("hashtree: chunk size %d must be positive", chunkSize)
+	}
 	if len(buf) == 0 {
 		return nil, errors.New("Empty data")
 	}
@@ -108,6 +178,8 @@ func NewHashTreeFromBuffer(buf []byte, chunkSize int) (*merkletree.MerkleTree, e
 	n := (len(buf) + chunkSize - 1) / chunkSize
 	leaves := make([]byte, 32*n)
 	root := make([]byte, 32)
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
 	rc := C.dm_root_buffer(c, unsafe.Pointer(&buf[0]), C.uint64_t(len(buf)), C.uint64_t(chunkSize),
 		(*C.uint8_t)(unsafe.Pointer(&leaves[0])), (*C.uint8_t)(unsafe.Pointer(&root[0])))
 	if rc != C.DM_OK {

@@ -8,7 +8,9 @@
 // coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h): calls
 // from concurrent handler goroutines go through one dm_batcher, which coalesces whatever is
 // queued into one batched GPU pass (dm_batcher_process), and dm_tree_levels builds the fid of
-// files larger than one window.  Swap it in by changing the handlers' import of
+// files larger than one window.  Go memory is bounded process-wide: 1 GiB per window of 8
+// segments in flight, DEOSS_PROCESS_MEM_GIB (default 8) windows at once across every upload,
+// buffers pooled, fragments written to disk as each window completes.  Swap it in by changing the handlers' import of
 // github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
 // Deviations: cipher must be "" (the AES branch is not implemented), and segment files are not
 // written (their bytes are the data fragments in order).  Build with `-tags hip`, CGO_ENABLED=1.
@@ -29,24 +31,45 @@ import (
 	"os"
 	"path/filepath"
 	"runtime"
+	"strconv"
 	"sync"
 	"unsafe"
 
 	"github.com/CESSProject/cess-go-sdk/chain"
 )
 
-// windowSegments is the number of segments coded per GPU call (2 GiB of file at 32 MiB).
-const windowSegments = 64
+// windowSegments segments go to the GPU per call: 8 x 32 MiB of file plus 8 x 12 x 8 MiB of
+// fragments = 1 GiB of Go memory per window.  A large file runs several windows at once (they
+// meet in the same dm_batcher pass, so the GPU still sees one wide batch), and every window in
+// flight, across all goroutines, holds one slot of the process-wide memory budget.
+const windowSegments = 8
 
 var (
 	once    sync.Once
 	ctx     *C.dm_ctx     // tree levels over the segment digests of multi-window files
 	batcher *C.dm_batcher // FullProcessing requests from every goroutine
 	initEr  error
+	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
+	bufs    sync.Pool     // *windowBuf, reused across calls
 )
+
+type windowBuf struct {
+	data, frags, segd, fragd []byte
+}
 
 func gpu() error {
 	once.Do(func() {
+		budget := 8
+		if v, err := strconv.Atoi(os.Getenv("DEOSS_PROCESS_MEM_GIB")); err == nil && v > 0 {
+			budget = v
+		}
+		slots = make(chan struct{}, budget)
+		seg, total := uint64(chain.SegmentSize), uint64(chain.DataShards+chain.ParShards)
+		frag := seg / uint64(chain.DataShards)
+		bufs.New = func() any {
+			return &windowBuf{data: make([]byte, windowSegments*seg), frags: make([]byte, windowSegments*total*frag),
+				segd: make([]byte, 32*windowSegments), fragd: make([]byte, 32*windowSegments*total)}
+		}
 		if rc := C.dm_create(&ctx, nil, 0); rc != C.DM_OK {
 			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
 			return
@@ -79,6 +102,50 @@ func ctxError(rc C.int) error {
 	return errors.New(C.GoString(C.dm_strerror(rc)))
 }
 
+// window is one GPU call's worth of the file: segments [first, first+nseg).
+type window struct {
+	first, nseg uint64
+	n           int // file bytes in the window
+	buf         *windowBuf
+	fid         [32]byte
+	err         error
+}
+
+// runWindow reads the window's bytes at its file offset, codes + hashes them through the batcher
+// and writes its fragments to savedir; the caller holds one budget slot.
+func runWindow(f *os.File, w *window, savedir string) {
+	seg := uint64(chain.SegmentSize)
+	total := uint64(chain.DataShards + chain.ParShards)
+	frag := seg / uint64(chain.DataShards)
+	b := bufs.Get().(*windowBuf)
+	w.buf = b
+	data := b.data[:w.n]
+	if _, err := f.ReadAt(data, int64(w.first*seg)); err != nil && err != io.EOF {
+		w.err = err
+		return
+	}
+	runtime.LockOSThread()
+	rc := C.dm_batcher_process(batcher, unsafe.Pointer(&data[0]), C.uint64_t(w.n), unsafe.Pointer(&b.frags[0]),
+		(*C.uint8_t)(unsafe.Pointer(&b.segd[0])), (*C.uint8_t)(unsafe.Pointer(&b.fragd[0])),
+		(*C.uint8_t)(unsafe.Pointer(&w.fid[0])))
+	if rc != C.DM_OK {
+		w.err = batcherError(rc)
+	}
+	runtime.UnlockOSThread()
+	if w.err != nil {
+		return
+	}
+	for t := uint64(0); t < w.nseg*total; t++ { // fragments go to disk before the buffer is reused
+		p := filepath.Join(savedir, hex.EncodeToString(b.fragd[32*t:32*t+32]))
+		if _, err := os.Stat(p); err != nil {
+			if err = os.WriteFile(p, b.frags[t*frag:(t+1)*frag], os.ModePerm); err != nil {
+				w.err = err
+				return
+			}
+		}
+	}
+}
+
 // FullProcessing cuts file into chain.SegmentSize segments (the last zero-padded), codes each into
 // chain.DataShards + chain.ParShards fragments written to savedir/<hex SHA-256>, and returns the
 // segment / fragment path names and the fid (hex hashtree root over the segments).
@@ -98,7 +165,8 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 	if err != nil {
 		return nil, "", err
 	}
-	if st.Size() == 0 {
+	size := uint64(st.Size())
+	if size == 0 {
 		return nil, "", errors.New("Empty data")
 	}
 	if err = os.MkdirAll(savedir, 0755); err != nil {
@@ -106,63 +174,58 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 	}
 	seg := uint64(chain.SegmentSize)
 	total := chain.DataShards + chain.ParShards
-	frag := seg / uint64(chain.DataShards)
-	wsize := windowSegments * seg // a small upload reads into a buffer of its own size
-	if uint64(st.Size()) < wsize {
-		wsize = uint64(st.Size())
+	nsegAll := (size + seg - 1) / seg
+	var wins []*window
+	for first := uint64(0); first < nsegAll; first += windowSegments {
+		nseg := min(uint64(windowSegments), nsegAll-first)
+		wins = append(wins, &window{first: first, nseg: nseg, n: int(min(nseg*seg, size-first*seg))})
 	}
-	window := make([]byte, wsize)
-	var info []chain.SegmentDataInfo
-	var segDigests []byte
-	var fid [32]byte
-	for {
-		n, rerr := io.ReadFull(f, window)
-		if n == 0 {
-			if rerr == io.EOF && len(info) == 0 {
-				return nil, "", errors.New("Empty data")
-			}
-			break
+	var wg sync.WaitGroup
+	for _, w := range wins { // windows run concurrently within the budget and batch together on the GPU
+		slots <- struct{}{}
+		wg.Add(1)
+		go func(w *window) {
+			defer wg.Done()
+			defer func() { <-slots }()
+			runWindow(f, w, savedir)
+		}(w)
+	}
+	wg.Wait()
+	info := make([]chain.SegmentDataInfo, 0, nsegAll)
+	segDigests := make([]byte, 0, 32*nsegAll)
+	var firstErr error
+	for _, w := range wins {
+		if w.err != nil && firstErr == nil {
+			firstErr = w.err
 		}
-		nseg := (uint64(n) + seg - 1) / seg
-		frags := make([]byte, nseg*uint64(total)*frag)
-		segd := make([]byte, 32*nseg)
-		fragd := make([]byte, 32*nseg*uint64(total))
-		runtime.LockOSThread()
-		rc := C.dm_batcher_process(batcher, unsafe.Pointer(&window[0]), C.uint64_t(n), unsafe.Pointer(&frags[0]),
-			(*C.uint8_t)(unsafe.Pointer(&segd[0])), (*C.uint8_t)(unsafe.Pointer(&fragd[0])),
-			(*C.uint8_t)(unsafe.Pointer(&fid[0])))
-		var perr error
-		if rc != C.DM_OK {
-			perr = batcherError(rc)
-		}
-		runtime.UnlockOSThread()
-		if perr != nil {
-			return nil, "", perr
-		}
-		for s := uint64(0); s < nseg; s++ {
-			names := make([]string, total)
-			for j := 0; j < total; j++ {
-				t := s*uint64(total) + uint64(j)
-				p := filepath.Join(savedir, hex.EncodeToString(fragd[32*t:32*t+32]))
-				if _, err := os.Stat(p); err != nil {
-					if err = os.WriteFile(p, frags[t*frag:(t+1)*frag], os.ModePerm); err != nil {
-						return nil, "", err
-					}
+		if firstErr == nil {
+			b := w.buf
+			for s := uint64(0); s < w.nseg; s++ {
+				names := make([]string, total)
+				for j := 0; j < total; j++ {
+					t := s*uint64(total) + uint64(j)
+					names[j] = filepath.Join(savedir, hex.EncodeToString(b.fragd[32*t:32*t+32]))
 				}
-				names[j] = p
+				info = append(info, chain.SegmentDataInfo{
+					SegmentHash:  filepath.Join(savedir, hex.EncodeToString(b.segd[32*s:32*s+32])),
+					FragmentHash: names,
+				})
 			}
-			info = append(info, chain.SegmentDataInfo{
-				SegmentHash:  filepath.Join(savedir, hex.EncodeToString(segd[32*s:32*s+32])),
-				FragmentHash: names,
-			})
+			segDigests = append(segDigests, b.segd[:32*w.nseg]...)
 		}
-		segDigests = append(segDigests, segd...)
-		if rerr != nil { // short final window
-			break
+		if w.buf != nil {
+			bufs.Put(w.buf)
+			w.buf = nil
 		}
 	}
-	if len(info) > windowSegments { // several windows: the fid is the tree over every segment
+	if firstErr != nil {
+		return nil, "", firstErr
+	}
+	fid := wins[0].fid
+	if len(wins) > 1 { // several windows: the fid is the tree over every segment
 		nodes := make([]byte, 32*uint64(C.dm_tree_node_count(C.uint64_t(len(info)))))
+		runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+		defer runtime.UnlockOSThread()
 		if rc := C.dm_tree_levels(ctx, (*C.uint8_t)(unsafe.Pointer(&segDigests[0])), C.uint64_t(len(info)),
 			(*C.uint8_t)(unsafe.Pointer(&nodes[0]))); rc != C.DM_OK {
 			return nil, "", ctxError(rc)

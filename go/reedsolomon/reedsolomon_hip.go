@@ -83,6 +83,8 @@ func New(dataShards, parityShards int, opts ...Option) (Encoder, error) {
 		return nil, err
 	}
 	r := &rsGPU{data: dataShards, parity: parityShards}
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	if rc := C.dm_rs_create(c, C.int(dataShards), C.int(parityShards), &r.h); rc != C.DM_OK {
 		return nil, errors.New(C.GoString(C.dm_last_error(c)))
 	}
@@ -146,6 +148,8 @@ func (r *rsGPU) Encode(shards [][]byte) error {
 	defer pin.Unpin()
 	arr, view := cPtrs(shards, &pin)
 	defer C.free(arr)
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	rc := C.dm_rs_encode(r.h, (*unsafe.Pointer)(unsafe.Pointer(&view[0])), (*unsafe.Pointer)(unsafe.Pointer(&view[r.data])),
 		C.uint64_t(size))
 	runtime.KeepAlive(shards)
@@ -166,6 +170,8 @@ func (r *rsGPU) Verify(shards [][]byte) (bool, error) {
 	arr, view := cPtrs(shards, &pin)
 	defer C.free(arr)
 	var ok C.int
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	rc := C.dm_rs_verify(r.h, (*unsafe.Pointer)(unsafe.Pointer(&view[0])), C.uint64_t(size), &ok)
 	runtime.KeepAlive(shards)
 	if rc != C.DM_OK {
@@ -205,6 +211,8 @@ func (r *rsGPU) Reconstruct(shards [][]byte) error {
 	defer C.free(arr)
 	cp := C.CBytes(present)
 	defer C.free(cp)
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
 	rc := C.dm_rs_reconstruct(r.h, (*unsafe.Pointer)(unsafe.Pointer(&view[0])), (*C.uint8_t)(cp), C.uint64_t(size))
 	runtime.KeepAlive(shards)
 	if rc != C.DM_OK {

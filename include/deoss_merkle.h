@@ -10,7 +10,9 @@
  * Conventions
  *  - Return codes: DM_OK (0) or a negative DM_ERR_*; dm_strerror() gives the message
  *    ("Empty data" for DM_ERR_EMPTY, matching common/hashtree/types.go:21), dm_last_error()
- *    the detailed message of the last failing call on a context.
+ *    the detailed message of the CALLING THREAD's last failing dm_* call (thread-local: no other
+ *    thread's failure can change or free it; every error return sets it, so it is never stale).
+ *    Go: hold runtime.LockOSThread across the failing call and the dm_last_error read.
  *  - Digests are the canonical 32-byte big-endian SHA-256 output.  Leaf digests are written
  *    n x 32 bytes in chunk order (leaf_out may be NULL).  merkletree's duplicated last leaf
  *    for odd n is NOT written (it equals leaf n-1).
@@ -53,12 +55,19 @@ enum {
 int dm_create(dm_ctx **out, const int *devs, int ndev);
 void dm_destroy(dm_ctx *ctx);
 const char *dm_strerror(int rc);
-const char *dm_last_error(dm_ctx *ctx);
+const char *dm_last_error(dm_ctx *ctx);   /* ctx is ignored (kept for ABI compatibility) */
 int dm_device_count(dm_ctx *ctx);
+/* GPUs visible to this process (HIP device count; 0 without a usable GPU).  Lets a binding
+ * default to every GPU of the node: dm_create(ctx, {0 .. dm_gpu_count()-1}, n). */
+int dm_gpu_count(void);
 
 /* ---- host-memory entry points (synchronous) ---------------------------------------------- */
 
-/* NewHashTree(chunkPath) (types.go:19-39): each file is one leaf, read whole. */
+/* NewHashTree(chunkPath) (types.go:19-39): each file is one leaf, read whole, in order, with Go's
+ * errors ("open <p>: no such file or directory", "read <p>: is a directory").  Streamed: files are
+ * pread straight into pinned staging by a few threads, H2D copies overlap the reads, and few long
+ * near-equal files (segment files) are hashed in stripes so every leaf chain runs while the rest
+ * is read.  With ndev > 1 the file list shards across the devices like dm_root_buffer. */
 int dm_new_hash_tree(dm_ctx *ctx, const char *const *paths, uint64_t n, uint8_t *leaf_out,
                      uint8_t root[32]);
 

@@ -279,3 +279,75 @@ void or_fill_splitmix(void *dst, uint64_t off, uint64_t nbytes, uint64_t seed) {
     uint64_t i0 = off / 8, nw = nbytes / 8;
     for (uint64_t i = 0; i < nw; i++) w[i] = splitmix64(seed ^ (i0 + i));
 }
+
+/* ---- root of a synthetic object that never exists in memory as a whole ----
+ * The object is bytes [0, len) of the splitmix64 stream `seed` (len a multiple of 8), split into
+ * `chunk`-byte leaves (chunk a multiple of 64).  Each thread takes whole leaves (atomic counter),
+ * regenerates a leaf's bytes 1 MiB at a time into its own buffer and feeds them to the compression
+ * function, so a 1 TiB object (BASELINE configs[3]) is checked with nthreads x 1 MiB of memory. */
+typedef struct {
+    uint64_t len, chunk, seed, n;
+    uint64_t next;           /* next leaf to take (atomic) */
+    uint8_t *leaf;
+} synth_job;
+
+static void synth_leaf(const synth_job *j, uint64_t i, uint8_t *buf, uint64_t bufsz) {
+    const uint64_t b0 = i * j->chunk;
+    const uint64_t l = (i + 1 < j->n) ? j->chunk : j->len - b0;
+    uint32_t st[8];
+    memcpy(st, IV256, sizeof st);
+    uint64_t done = 0;
+    while (done + 64 <= l) {   /* whole blocks, bufsz (a multiple of 64) at a time */
+        uint64_t take = l - done < bufsz ? (l - done) / 64 * 64 : bufsz;
+        or_fill_splitmix(buf, b0 + done, take, j->seed);
+        compress(st, buf, take / 64);
+        done += take;
+    }
+    uint8_t tail[128];
+    const uint64_t r = l - done;   /* < 64, a multiple of 8 */
+    memset(tail, 0, sizeof tail);
+    if (r) or_fill_splitmix(tail, b0 + done, r, j->seed);
+    tail[r] = 0x80;
+    const uint64_t tb = (r + 9 <= 64) ? 64 : 128, bits = l * 8;
+    for (int k = 0; k < 8; k++) tail[tb - 1 - k] = (uint8_t)(bits >> (8 * k));
+    compress(st, tail, tb / 64);
+    uint8_t *out = j->leaf + 32 * i;
+    for (int k = 0; k < 8; k++) {
+        out[4 * k] = (uint8_t)(st[k] >> 24); out[4 * k + 1] = (uint8_t)(st[k] >> 16);
+        out[4 * k + 2] = (uint8_t)(st[k] >> 8); out[4 * k + 3] = (uint8_t)st[k];
+    }
+}
+
+static void *synth_worker(void *arg) {
+    synth_job *j = (synth_job *)arg;
+    const uint64_t bufsz = 1u << 20;
+    uint8_t *buf = (uint8_t *)malloc(bufsz);
+    for (;;) {
+        uint64_t i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (i >= j->n) break;
+        synth_leaf(j, i, buf, bufsz);
+    }
+    free(buf);
+    return NULL;
+}
+
+/* Returns -1 for len 0, -2 for a bad chunk/len, else 0; leaf_out (nullable) gets n x 32 bytes. */
+int or_root_synthetic(uint64_t len, uint64_t chunk, uint64_t seed, uint8_t *leaf_out, uint8_t root[32],
+                      int nthreads) {
+    if (len == 0) return -1;
+    if (chunk == 0 || chunk % 64 || len % 8) return -2;
+    synth_job j = {len, chunk, seed, (len + chunk - 1) / chunk, 0, NULL};
+    j.leaf = leaf_out ? leaf_out : (uint8_t *)malloc(32 * j.n);
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    if ((uint64_t)nthreads > j.n) nthreads = (int)j.n;
+    pthread_t th[256];
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, synth_worker, &j);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    uint8_t *tmp = (uint8_t *)malloc(32 * j.n);
+    or_reduce(j.leaf, j.n, -1, tmp);
+    memcpy(root, tmp, 32);
+    free(tmp);
+    if (!leaf_out) free(j.leaf);
+    return 0;
+}

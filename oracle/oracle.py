@@ -307,6 +307,7 @@ class Oracle:
         L.or_root_chunks.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(u64), u64, vp, vp, ctypes.c_int]
         L.or_root_buffer.argtypes = [vp, u64, u64, vp, vp, ctypes.c_int]
         L.or_fill_splitmix.argtypes = [vp, u64, u64, u64]
+        L.or_root_synthetic.argtypes = [u64, u64, u64, vp, vp, ctypes.c_int]
         L.or_set_backend.argtypes = [ctypes.c_int]
         L.or_rs_matrix.argtypes = [ctypes.c_int, ctypes.c_int, vp]
         L.or_rs_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -367,6 +368,20 @@ class Oracle:
         b = ctypes.create_string_buffer(bytes(buf), max(len(buf), 1))
         leaves, root = self.root_buffer_ptr(ctypes.addressof(b), len(buf), chunk, nthreads, True)
         return leaves, root
+
+    def root_synthetic(self, length: int, chunk: int, seed: int, nthreads: int = 1,
+                       want_leaves: bool = False) -> Tuple[Optional[bytes], bytes]:
+        """Root of bytes [0, length) of the splitmix64 stream `seed`, regenerated leaf by leaf
+        (no whole-object buffer: the 1 TiB configs[3] check)."""
+        n = (length + chunk - 1) // chunk if length else 0
+        leaf = ctypes.create_string_buffer(max(32 * n, 32)) if want_leaves else None
+        root = ctypes.create_string_buffer(32)
+        rc = self.L.or_root_synthetic(length, chunk, seed, leaf, root, nthreads)
+        if rc == -1:
+            raise ValueError("Empty data")
+        if rc != 0:
+            raise ValueError(f"or_root_synthetic rc={rc} (chunk must be a multiple of 64, length of 8)")
+        return (leaf.raw[:32 * n] if leaf is not None else None), root.raw
 
     def fill_splitmix_ptr(self, addr: int, off: int, nbytes: int, seed: int) -> None:
         assert off % 8 == 0 and nbytes % 8 == 0

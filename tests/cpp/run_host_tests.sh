@@ -10,7 +10,7 @@ INC="-I include -I /opt/rocm/include -D__HIP_PLATFORM_AMD__"
 LIBS="-L oracle -loracle_merkle -L /opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,$PWD/oracle:/opt/rocm/lib"
 # (1) plain
 g++ -O2 -std=c++17 $INC tests/cpp/test_capi_host.cpp -L deoss_amd -ldeoss_merkle -Wl,-rpath,$PWD/deoss_amd $LIBS -o $out/test_plain
-$out/test_plain
+$out/test_plain $out
 # (2) sanitized host code
 hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -I include \
   -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer \
@@ -19,4 +19,4 @@ hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -I include \
 /opt/rocm/lib/llvm/bin/clang++ -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $INC tests/cpp/test_capi_host.cpp \
   -L $out -ldeoss_merkle_asan -Wl,-rpath,$out $LIBS -o $out/test_asan
 ASAN_OPTIONS=detect_leaks=0:protect_shadow_gap=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 \
-  $out/test_asan
+  $out/test_asan $out

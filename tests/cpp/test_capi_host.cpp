@@ -6,6 +6,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <fstream>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -29,7 +30,7 @@ uint64_t or_reduce(const uint8_t* digests, uint64_t n, int levels, uint8_t* out)
 void or_sha256(const void* data, uint64_t len, uint8_t out[32]);
 }
 
-static int fails = 0;
+static std::atomic<int> fails{0};
 #define EXPECT(c)                                                                     \
     do {                                                                              \
         if (!(c)) {                                                                   \
@@ -107,7 +108,67 @@ static void check_buffer(dm_ctx* c, uint64_t len, uint64_t chunk, uint64_t seed)
     }
 }
 
-int main() {
+// Write files under dir, return their paths (the NewHashTree inputs).
+static std::vector<std::string> write_files(const std::string& dir, const std::vector<std::vector<uint8_t>>& data,
+                                            const char* tag) {
+    std::vector<std::string> paths;
+    for (size_t i = 0; i < data.size(); i++) {
+        paths.push_back(dir + "/" + tag + std::to_string(i));
+        std::ofstream f(paths.back(), std::ios::binary);
+        f.write(reinterpret_cast<const char*>(data[i].data()), (std::streamsize)data[i].size());
+    }
+    return paths;
+}
+
+// dm_new_hash_tree over files vs or_root_chunks over the same bytes (leaves and root).
+static void check_files(dm_ctx* c, const std::string& dir, const std::vector<std::vector<uint8_t>>& data,
+                        const char* tag) {
+    auto paths = write_files(dir, data, tag);
+    std::vector<const char*> cp;
+    std::vector<const void*> ptrs;
+    std::vector<uint64_t> lens;
+    for (size_t i = 0; i < data.size(); i++) {
+        cp.push_back(paths[i].c_str());
+        ptrs.push_back(data[i].data());
+        lens.push_back(data[i].size());
+    }
+    const uint64_t n = data.size();
+    std::vector<uint8_t> lw(32 * n), lg(32 * n);
+    uint8_t rw[32], rg[32];
+    EXPECT(or_root_chunks(ptrs.data(), lens.data(), n, lw.data(), rw, 4) == 0);
+    EXPECT(dm_new_hash_tree(c, cp.data(), n, lg.data(), rg) == DM_OK);
+    EXPECT(std::memcmp(rw, rg, 32) == 0 && lw == lg);
+    for (auto& p : paths) std::remove(p.c_str());
+}
+
+// The Go Stream call sequence (go/hashtree/stream_hip.go): NewStream, Write pieces of random
+// sizes, Close with leaf_cap = ceil(received / chunk); or Abort mid-body.
+static void go_stream_sequence(dm_ctx* c, uint64_t len, uint64_t chunk, uint64_t seed, bool abort_midway) {
+    auto b = bytes(len, seed);
+    dm_stream* st = nullptr;
+    EXPECT(dm_stream_open(c, chunk, &st) == DM_OK);
+    std::mt19937_64 rng(seed * 31 + 7);
+    uint64_t pos = 0;
+    while (pos < len) {
+        const uint64_t m = std::min<uint64_t>(len - pos, 1 + rng() % (2u << 20));
+        EXPECT(dm_stream_write(st, b.data() + pos, m) == DM_OK);
+        pos += m;
+        if (abort_midway && pos > len / 2) {
+            dm_stream_abort(st);
+            return;
+        }
+    }
+    const uint64_t n = (len + chunk - 1) / chunk;
+    std::vector<uint8_t> lw(32 * n), lg(32 * n);
+    uint8_t rw[32], rg[32];
+    uint64_t got = 0;
+    EXPECT(or_root_buffer(b.data(), len, chunk, lw.data(), rw, 2) == 0);
+    EXPECT(dm_stream_close(st, lg.data(), n, &got, rg) == DM_OK);
+    EXPECT(got == n && std::memcmp(rw, rg, 32) == 0 && lw == lg);
+}
+
+int main(int argc, char** argv) {
+    const std::string tmpdir = argc > 1 ? argv[1] : "/tmp";
     dm_ctx* c = nullptr;
     int rc = dm_create(&c, nullptr, 0);
     if (rc != DM_OK) {
@@ -405,6 +466,95 @@ int main() {
                DM_ERR_INVALID);
     }
 
+    // dm_last_error: the calling thread's last failure, never another thread's, never stale
+    {
+        EXPECT(dm_root_buffer(c, nullptr, 0, 64, nullptr, root) == DM_ERR_EMPTY);
+        std::thread other([c] {
+            uint8_t r[32];
+            const char* gone[] = {"/nonexistent/other/thread"};
+            EXPECT(dm_new_hash_tree(c, gone, 1, nullptr, r) == DM_ERR_IO);
+            EXPECT(std::string(dm_last_error(c)).find("/nonexistent/other/thread") != std::string::npos);
+        });
+        other.join();
+        EXPECT(std::string(dm_last_error(c)) == "Empty data");
+        EXPECT(dm_root_buffer(c, root, 1, 0, nullptr, root) == DM_ERR_INVALID);
+        EXPECT(std::string(dm_last_error(c)) == "invalid argument");
+    }
+
+    // NewHashTree from files: Go's error order and text, packed and striped layouts
+    {
+        const std::string d = tmpdir;
+        const std::vector<std::vector<uint8_t>> two = {bytes(10, 1), bytes(20, 2)};
+        auto paths = write_files(d, two, "err");
+        std::string miss = d + "/missing_file_x";
+        const char* order[] = {paths[0].c_str(), d.c_str(), miss.c_str(), paths[1].c_str()};
+        EXPECT(dm_new_hash_tree(c, order, 4, nullptr, root) == DM_ERR_IO);   // the directory comes first
+        EXPECT(std::string(dm_last_error(c)) == "read " + d + ": is a directory");
+        const char* order2[] = {paths[0].c_str(), miss.c_str(), d.c_str()};
+        EXPECT(dm_new_hash_tree(c, order2, 3, nullptr, root) == DM_ERR_IO);
+        EXPECT(std::string(dm_last_error(c)) == "open " + miss + ": no such file or directory");
+        for (auto& p : paths) std::remove(p.c_str());
+        std::vector<std::vector<uint8_t>> small;
+        for (int i = 0; i < 300; i++) small.push_back(bytes((uint64_t)(i * 7919) % 70000, 4000 + i));   // incl. 0 B
+        check_files(c, d, small, "small");
+        std::vector<std::vector<uint8_t>> segs;   // 12 near-equal 24 MiB files: 288 MiB, striped
+        for (int i = 0; i < 12; i++) segs.push_back(bytes((24u << 20) - (i == 11 ? 12345 : 0), 6000 + i));
+        check_files(c, d, segs, "seg");
+        segs.resize(5);                          // 5 x 24 MiB: 120 MiB, packed through the pinned ring
+        check_files(c, d, segs, "seg5_");
+    }
+
+    // ndev > 1 semantics on this box's one GPU (DEOSS_FORCE_SHARDED): block partition, RCCL
+    // all-gather, leaf_out at odd and even n, an async call of the same context queued first
+    {
+        setenv("DEOSS_FORCE_SHARDED", "1", 1);
+        dm_ctx* cs = nullptr;
+        EXPECT(dm_create(&cs, nullptr, 0) == DM_OK);
+        unsetenv("DEOSS_FORCE_SHARDED");
+        if (cs) {
+            for (auto [len, chunk] : {std::pair<uint64_t, uint64_t>{1000ull * 4096, 4096},       // n = 1000 (even)
+                                      {1001ull * 4096 - 7, 4096},                                 // n = 1001 (odd)
+                                      {(300ull << 20) + 5, 32ull << 20},                          // 10 striped leaves
+                                      {3 * 64, 64}}) {
+                auto b = bytes(len, len + 3);
+                const uint64_t n = (len + chunk - 1) / chunk;
+                // async root of another object on the null stream, enqueued before the sharded call
+                auto other = bytes(5u << 20, 77);
+                void* dev = nullptr;
+                void* droot = nullptr;
+                EXPECT(hipMalloc(&dev, other.size() + 64) == hipSuccess && hipMalloc(&droot, 32) == hipSuccess);
+                EXPECT(hipMemcpy(dev, other.data(), other.size(), hipMemcpyHostToDevice) == hipSuccess);
+                EXPECT(dm_root_device_async(cs, dev, other.size(), 1 << 16, droot, nullptr, nullptr) == DM_OK);
+                std::vector<uint8_t> lw(32 * n), lg(32 * n);
+                uint8_t rw[32], rg[32], ro[32], rd[32];
+                EXPECT(or_root_buffer(b.data(), len, chunk, lw.data(), rw, 4) == 0);
+                EXPECT(dm_root_buffer(cs, b.data(), len, chunk, lg.data(), rg) == DM_OK);
+                EXPECT(std::memcmp(rw, rg, 32) == 0 && lw == lg);
+                EXPECT(hipDeviceSynchronize() == hipSuccess);
+                EXPECT(hipMemcpy(rd, droot, 32, hipMemcpyDeviceToHost) == hipSuccess);
+                EXPECT(or_root_buffer(other.data(), other.size(), 1 << 16, nullptr, ro, 2) == 0);
+                EXPECT(std::memcmp(ro, rd, 32) == 0);
+                (void)hipFree(dev);
+                (void)hipFree(droot);
+            }
+            std::vector<std::vector<uint8_t>> files;
+            for (int i = 0; i < 37; i++) files.push_back(bytes(1000 + (uint64_t)i * 333, 7000 + i));
+            check_files(cs, tmpdir, files, "shard");
+            dm_destroy(cs);
+        }
+    }
+
+    // the Go Stream call sequence: random pieces, an aborted body, concurrent uploads
+    go_stream_sequence(c, (9u << 20) + 123, 1u << 20, 11, false);
+    go_stream_sequence(c, (40u << 20) + 5, 32u << 20, 12, false);
+    go_stream_sequence(c, 10u << 20, 1u << 16, 13, true);
+    {
+        std::vector<std::thread> ups;
+        for (int t = 0; t < 6; t++)
+            ups.emplace_back([c, t] { go_stream_sequence(c, 3000000 + 4097 * t, 65536, 50 + t, t == 3); });
+        for (auto& x : ups) x.join();
+    }
+
     // concurrent callers on one context
     std::vector<std::thread> th;
     for (int t = 0; t < 4; t++) th.emplace_back([c, t] { check_buffer(c, 200000 + 1111 * t, 4096, 900 + t); });
@@ -412,7 +562,7 @@ int main() {
 
     dm_destroy(c);
     if (fails) {
-        std::fprintf(stderr, "%d failures\n", fails);
+        std::fprintf(stderr, "%d failures\n", fails.load());
         return 1;
     }
     std::printf("PASS\n");

@@ -28,8 +28,36 @@ def chunk_bytes(spec):
     return splitmix64_bytes(spec["len"], spec["seed"])
 
 
+def splitmix64_np(nbytes: int, seed: int, off: int = 0):
+    """Vectorised splitmix64 stream (same function as oracle.splitmix64_bytes, checked against it
+    below) so the full-size BASELINE config roots can be generated in seconds."""
+    import numpy as np
+    i = np.arange(off // 8, (off + nbytes + 7) // 8, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) ^ i) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z.astype("<u8").tobytes()[:nbytes]
+
+
+def synthetic_object_root(length: int, chunk: int, seed: int):
+    """Leaf digests + root of bytes [0, length) of the splitmix64 stream, leaf by leaf (hashlib)."""
+    piece = 1 << 24
+    leaves = []
+    for b0 in range(0, length, chunk):
+        h = hashlib.sha256()
+        end = min(length, b0 + chunk)
+        for p in range(b0, end, piece):
+            h.update(splitmix64_np(min(piece, end - p), seed, p))
+        leaves.append(h.digest())
+    from oracle import py_reduce
+    return leaves, py_reduce(leaves)[0]
+
+
 def main() -> None:
     cases = []
+    assert splitmix64_np(1000, 12345, 8) == splitmix64_bytes(1000, 12345, 8)
     # 1. reference KAT (hashtree_test.go:20-82), expected values built exactly like the test:
     #    root = SHA256( SHA256(L0||L1) || SHA256(L2||L3) )
     texts = ["content_one", "content_two", "content_three", "content_four"]
@@ -89,6 +117,16 @@ def main() -> None:
         roots.append(py_root_chunks(data)[1].hex())
     cases.append({"name": "batch_10_objects", "kind": "batch", "objects": objs, "chunk": chunk,
                   "roots": roots, "pinned": "restatement"})
+    # 6. BASELINE configs at full size (seeds 0xDE0550000 + k):
+    #    configs[0] = one 64 MiB object at 32 MiB chunks (2 leaves; the CPU plumbing config),
+    #    configs[1] = one 8 GiB object at 32 MiB chunks (256 leaves; the bench headline).
+    for k, length in ((0, 64 << 20), (1, 8 << 30)):
+        s = seed + k if k == 0 else seed + 2      # bench.py SEED = 0xDE0550002 for configs[1]
+        leaves, r = synthetic_object_root(length, 32 << 20, s)
+        cases.append({"name": f"config{k}_{length >> 20}MiB_chunk32MiB", "kind": "buffer", "len": length,
+                      "chunk": 32 << 20, "seed": s, "n_leaves": len(leaves), "root": r.hex(),
+                      "leaves_sha256": hashlib.sha256(b"".join(leaves)).hexdigest(),
+                      "pinned": "restatement", "full_size": True})
     with open(OUT, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py (Python hashlib restatement)",
                    "synthetic": "word[i] = splitmix64(seed ^ i), little-endian", "cases": cases}, f, indent=0)

@@ -110,7 +110,7 @@ def test_golden_chunks(ctx, golden, leaf_mode):
 
 def test_golden_buffers_all_paths(ctx, golden, leaf_mode):
     for case in golden:
-        if case["kind"] != "buffer":
+        if case["kind"] != "buffer" or case.get("full_size"):
             continue
         buf = splitmix64_bytes(case["len"], case["seed"])
         n, chunk = case["n_leaves"], case["chunk"]
@@ -128,6 +128,23 @@ def test_golden_buffers_all_paths(ctx, golden, leaf_mode):
             assert r.hex() == case["root"], (case["name"], off)
             assert lv[:32 * n] == leaves, (case["name"], off)
         assert ctx.root_device(ptr, len(buf), chunk).hex() == case["root"]
+
+
+@pytest.mark.parametrize("name", ["config0_64MiB_chunk32MiB", "config1_8192MiB_chunk32MiB"])
+def test_full_size_config_roots(ctx, golden, name):
+    """BASELINE configs[0] / configs[1] at full size in HBM (device generator, auto leaf kernel)
+    against the hashlib-generated fixture root and leaf digests."""
+    torch = _torch()
+    case = next(c for c in golden if c["name"] == name)
+    length, chunk = case["len"], case["chunk"]
+    buf = torch.empty(length + 64, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, length, case["seed"], s)
+    got, lv = root_dev(ctx, buf.data_ptr(), length, chunk, want_leaves=True)
+    assert got.hex() == case["root"]
+    assert hashlib.sha256(lv).hexdigest() == case["leaves_sha256"]
+    del buf
+    torch.cuda.empty_cache()
 
 
 def test_golden_batch(ctx, golden, leaf_mode):
@@ -260,24 +277,112 @@ def test_sharded_subtrees_match_full_root(ctx, oracle_lib, world, leaf_mode):
         assert bytes(root.cpu().numpy()) == want, (length, chunk, world)
 
 
-def test_single_process_sharded_path(oracle_lib):
-    """dm_create's multi-device path (aligned block partition, ncclAllGather of subtree roots,
-    compaction, final levels) forced on the one GPU of this box via DEOSS_FORCE_SHARDED."""
+def _forced_sharded_context():
     from deoss_amd import MerkleContext
     os.environ["DEOSS_FORCE_SHARDED"] = "1"
     try:
-        c = MerkleContext()
+        return MerkleContext()
     finally:
         del os.environ["DEOSS_FORCE_SHARDED"]
+
+
+def test_single_process_sharded_path(oracle_lib):
+    """dm_create's multi-device path (aligned block partition, ncclAllGather of subtree roots,
+    compaction, final levels) forced on the one GPU of this box via DEOSS_FORCE_SHARDED: leaf
+    digests from the same pass at odd and even n, striped H2D for few long leaves, and an async
+    call of the same context queued on the null stream just before each sharded call."""
+    torch = _torch()
+    c = _forced_sharded_context()
+    other = oracle_lib.splitmix_bytes(5 << 20, 77)
+    _, want_other = oracle_lib.root_buffer(other, 1 << 16)
+    t_other, p_other = dev_bytes(other)
     try:
-        for length, chunk in [(1000 * 4096 + 7, 4096), (3 * 64, 64), (5000, 1000), ((1 << 20) + 3, 1 << 14)]:
+        for length, chunk in [(1000 * 4096 + 7, 4096), (1000 * 4096, 4096), (3 * 64, 64), (4 * 64, 64),
+                              (5000, 1000), ((1 << 20) + 3, 1 << 14), ((300 << 20) + 5, 32 << 20)]:
             host = oracle_lib.splitmix_bytes(length, length + 1)
-            lw, want = oracle_lib.root_buffer(host, chunk)
+            lw, want = oracle_lib.root_buffer(host, chunk, nthreads=8)
+            r = torch.zeros(32, dtype=torch.uint8, device="cuda")
+            c.root_device_async(p_other, len(other), 1 << 16, r.data_ptr(), 0, 0)
             leaves, root = c.root_buffer(host, chunk, want_leaves=True)
+            torch.cuda.synchronize()
             assert root == want, (length, chunk)
             assert leaves == lw, (length, chunk)
+            assert bytes(r.cpu().numpy()) == want_other, (length, chunk)
     finally:
         c.close()
+
+
+def _write_files(tmp_path, datas, tag):
+    paths = []
+    for i, d in enumerate(datas):
+        p = tmp_path / f"{tag}{i}"
+        p.write_bytes(d)
+        paths.append(str(p))
+    return paths
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_new_hash_tree_files_layouts(ctx, oracle_lib, tmp_path, sharded, leaf_mode):
+    """dm_new_hash_tree (NewHashTree(chunkPath), types.go:19-39) from files: packed layout (many /
+    small files, empty files), striped layout (few long near-equal files > 256 MiB in total), and
+    the multi-device partition of the file list (forced on one GPU)."""
+    c = _forced_sharded_context() if sharded else ctx
+    if sharded:
+        c.set_leaf_kernel(leaf_mode)
+    try:
+        cases = [
+            ("small", [oracle_lib.splitmix_bytes((i * 7919) % 70000, 4000 + i) for i in range(300)]),
+            ("seg", [oracle_lib.splitmix_bytes((24 << 20) - (12345 if i == 11 else 0), 6000 + i) for i in range(12)]),
+            ("five", [oracle_lib.splitmix_bytes(24 << 20, 7000 + i) for i in range(5)]),
+            ("odd", [oracle_lib.splitmix_bytes(n, 8000 + n) for n in (0, 1, 63, 64, 65, 4096, 100000)]),
+        ]
+        for tag, datas in cases:
+            paths = _write_files(tmp_path, datas, tag)
+            lw, want = oracle_lib.root_chunks(datas, nthreads=8)
+            leaves, root = c.new_hash_tree(paths)
+            assert root == want, tag
+            assert b"".join(leaves) == lw, tag
+            for p in paths:
+                os.remove(p)
+    finally:
+        if sharded:
+            c.close()
+
+
+def test_new_hash_tree_go_errors(ctx, tmp_path):
+    """types.go:24-33 reads files in order and returns the first failure, with Go's text."""
+    from deoss_amd import DeossMerkleError
+    a, b = _write_files(tmp_path, [b"x" * 10, b"y" * 20], "e")
+    miss = str(tmp_path / "missing")
+    with pytest.raises(DeossMerkleError) as e:
+        ctx.new_hash_tree([a, str(tmp_path), miss, b])
+    assert str(e.value) == f"read {tmp_path}: is a directory"
+    with pytest.raises(DeossMerkleError) as e:
+        ctx.new_hash_tree([a, miss, str(tmp_path)])
+    assert str(e.value) == f"open {miss}: no such file or directory"
+
+
+def test_last_error_is_per_thread(ctx):
+    """dm_last_error is the calling thread's last failure: another thread failing meanwhile does
+    not change (or free) it, and argument errors never leave an older message behind."""
+    from deoss_amd import DeossMerkleError
+    L = ctx._L
+    import ctypes as ct
+    root = ct.create_string_buffer(32)
+    assert L.dm_root_buffer(ctx._h, None, 0, 64, None, root) == -1
+    seen = []
+
+    def other():
+        with pytest.raises(DeossMerkleError):
+            ctx.new_hash_tree(["/nonexistent/other/thread"])
+        seen.append(L.dm_last_error(ctx._h))
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert b"/nonexistent/other/thread" in seen[0]
+    assert L.dm_last_error(ctx._h) == b"Empty data"
+    assert L.dm_root_buffer(ctx._h, root, 1, 0, None, root) == -2
+    assert L.dm_last_error(ctx._h) == b"invalid argument"
 
 
 # ---------------------------------------------------------------- host buffer e2e (stripes)

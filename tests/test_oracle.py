@@ -86,6 +86,8 @@ def test_reduce_exact_levels_compose():
 
 def test_golden_fixtures_match_oracles(golden, oracle_lib):
     for case in golden:
+        if case.get("full_size"):
+            continue    # test_full_size_config_fixtures
         if case["kind"] == "chunks":
             data = chunks_of(case)
             leaves, root = py_root_chunks(data)
@@ -132,3 +134,30 @@ def test_splitmix_offsets(oracle_lib):
     part = oracle_lib.splitmix_bytes(1 << 12, 5, off=1 << 15)
     assert full[1 << 15:(1 << 15) + (1 << 12)] == part
     assert splitmix64_bytes(1 << 12, 5, off=1 << 15) == part
+
+
+@pytest.mark.parametrize("name", ["config0_64MiB_chunk32MiB", "config1_8192MiB_chunk32MiB"])
+def test_full_size_config_fixtures(golden, oracle_lib, name):
+    """BASELINE configs[0] (64 MiB) and configs[1] (8 GiB) at full size: the C restatement,
+    regenerating the synthetic bytes leaf by leaf (or_root_synthetic, the configs[3] checker),
+    reproduces the hashlib-generated fixture roots and leaf digests."""
+    case = next(c for c in golden if c["name"] == name)
+    leaves, root = oracle_lib.root_synthetic(case["len"], case["chunk"], case["seed"], nthreads=8,
+                                             want_leaves=True)
+    assert root.hex() == case["root"]
+    assert hashlib.sha256(leaves).hexdigest() == case["leaves_sha256"]
+    if case["len"] <= (64 << 20):   # the buffer form agrees too
+        buf = oracle_lib.splitmix_bytes(case["len"], case["seed"])
+        assert oracle_lib.root_buffer(buf, case["chunk"], nthreads=2)[1].hex() == case["root"]
+
+
+def test_root_synthetic_matches_buffer(oracle_lib):
+    for length, chunk in [(8, 64), (64 * 1000 + 8, 64), (3 << 20, 1 << 20), ((5 << 20) + 24, 1 << 20),
+                          (4096 * 7 + 64, 4096), (1 << 16, 1 << 16)]:
+        a = oracle_lib.root_synthetic(length, chunk, 77, nthreads=3, want_leaves=True)
+        b = oracle_lib.root_buffer(oracle_lib.splitmix_bytes(length, 77), chunk, nthreads=2)
+        assert a == b, (length, chunk)
+    with pytest.raises(ValueError, match="Empty data"):
+        oracle_lib.root_synthetic(0, 64, 1)
+    with pytest.raises(ValueError):
+        oracle_lib.root_synthetic(64, 100, 1)
