@@ -93,6 +93,9 @@ def main() -> None:
     ap.add_argument("--piece-kib", type=int, default=1024, help="upload: bytes per dm_stream_write (KiB)")
     ap.add_argument("--segment-mib", type=int, default=32, help="rs: segment bytes (chain.SegmentSize)")
     ap.add_argument("--objects", type=int, default=4096, help="batch/stream: objects per GPU")
+    ap.add_argument("--total-objects", type=int, default=0,
+                    help="batch/stream: objects across all ranks, split evenly (100000 x 1 MiB at --gpus 8 = "
+                         "BASELINE configs[4]: 12,500 per GPU); 0 = --objects per GPU")
     ap.add_argument("--object-mib", type=float, default=4.0, help="batch/stream: object size (MiB)")
     ap.add_argument("--threads", type=int, default=256, help="concurrent: caller threads")
     ap.add_argument("--mode", default="root", choices=["root", "process"], help="concurrent: request kind")
@@ -940,12 +943,16 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
     from deoss_amd import MerkleContext
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     obj = int(args.object_mib * (1 << 20))
-    nobj = args.objects
+    if args.total_objects:   # replicas: rank r takes objects [T*r/N, T*(r+1)/N), no exchange
+        nobj = args.total_objects * (rank + 1) // world - args.total_objects * rank // world
+    else:
+        nobj = args.objects
     chunk = args.chunk
     ctx = MerkleContext(devices=[dev_index])
     ctx.set_leaf_kernel(args.leaf_kernel)
     sptr = torch.cuda.current_stream().cuda_stream
-    seed0 = SEED + 1000 * (rank + 1)
+    first = args.total_objects * rank // world if args.total_objects else rank * nobj
+    seed0 = SEED + 1000 + first     # object g of the whole job: its own splitmix64 stream
     total_local = obj * nobj
     pitch = (obj + 255) // 256 * 256
     buf = torch.empty(pitch * nobj + 64, dtype=torch.uint8, device=device)
@@ -1016,15 +1023,28 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
     out = {
         "metric": "device-resident GiB/s hashed to Merkle root; 1/2/4/8 MI355X scaling" if args.workload == "batch"
         else "host-resident GiB/s hashed to Merkle roots (pinned H2D inside the timed region)",
-        "value": round(total_local * world * args.steps / elapsed / (1 << 30), 4), "unit": "GiB/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "value": round((obj * args.total_objects if args.total_objects else total_local * world) * args.steps
+                       / elapsed / (1 << 30), 4), "unit": "GiB/s",
+        "n_gpus": 1 if args.same_device else world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong" if args.total_objects else "weak",
         "vs_baseline": None, "dtype": "u32", "data": "synthetic splitmix64 objects",
-        "config": {"workload": f"{nobj} objects x {obj} B per GPU ({args.workload}), chunk {chunk}",
-                   "objects_per_gpu": nobj, "object_bytes": obj, "chunk": chunk, "leaf_kernel": kind},
+        "config": {"workload": (f"{args.total_objects} objects x {obj} B over {world} rank(s) ({args.workload}), "
+                                f"chunk {chunk}" if args.total_objects else
+                                f"{nobj} objects x {obj} B per GPU ({args.workload}), chunk {chunk}"),
+                   "objects_per_gpu": nobj, "object_bytes": obj, "chunk": chunk, "leaf_kernel": kind,
+                   "parallelism": f"{world} replica(s), objects split across ranks, no exchange"},
         "k1_avg_ms": round(k1_ms_sum / max(ncalls, 1), 4), "call_avg_ms": round(call_ms_sum / max(ncalls, 1), 4),
         "parity": {"checked_objects": check, "mismatches": int(mism), "bit_exact": mism == 0},
     }
+    if args.same_device:
+        out.update({"ranks": world, "same_device": True,
+                    "note": "rehearsal: every rank on cuda:0 of one GPU; not a multi-GPU result"})
+    if world > 1:   # every rank's roots were checked against the CPU: report all ranks' mismatches
+        t = torch.tensor([mism, check], dtype=torch.int64, device="cpu" if gloo else device)
+        dist.all_reduce(t)
+        out["parity"] = {"checked_objects": int(t[1]), "mismatches": int(t[0]), "bit_exact": int(t[0]) == 0,
+                         "ranks": world}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

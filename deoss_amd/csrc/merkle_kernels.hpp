@@ -92,9 +92,38 @@ __device__ __forceinline__ void block_words(const Blk& b, uint32_t (&w)[16]) {
 // Absorb nb full blocks starting at p, the next block's loads in flight during each
 // compression (register double buffer).  A paired 128-byte variant was measured to make hipcc
 // sink the prefetch next to its use (DESIGN.md "K1"), so blocks stay 64 bytes per iteration.
+#ifndef DM_K1_LINES
+#define DM_K1_LINES 1
+#endif
 template <bool ALIGNED>
 __device__ __forceinline__ void absorb_blocks(uint32_t (&st)[8], const uint8_t* p, uint64_t nb) {
     if (nb == 0) return;
+    if constexpr (ALIGNED && DM_K1_LINES) {
+        // Whole 128-byte lines: each iteration absorbs two blocks and issues all eight 16-B loads
+        // of the NEXT line at once, so every L2 line a lane touches is consumed in one go.  With
+        // one block (half a line) per iteration the second half was requested ~1,400 instructions
+        // later, after ~24 waves per CU had pulled their own lines through the 4 MiB XCD L2, and
+        // 36 % of the lines were fetched twice at 64 KiB chunks (profiles/k1_traffic.json).
+        // Loads past the leaf's last block re-read that block (already in cache): no branches
+        // around the loads, so they issue as one burst.
+        const uint64_t last = nb - 1;
+        Blk c0 = load_block<true>(p), c1 = load_block<true>(p + 64 * (last < 1 ? last : 1));
+        for (uint64_t b = 0; b < nb; b += 2) {
+            const uint64_t b2 = b + 2 < last ? b + 2 : last, b3 = b + 3 < last ? b + 3 : last;
+            const Blk n0 = load_block<true>(p + 64 * b2), n1 = load_block<true>(p + 64 * b3);
+            __builtin_amdgcn_sched_barrier(0);   // the next line's loads stay ahead of the rounds
+            uint32_t w[16];
+            block_words(c0, w);
+            compress(st, w);
+            if (b + 1 < nb) {
+                block_words(c1, w);
+                compress(st, w);
+            }
+            c0 = n0;
+            c1 = n1;
+        }
+        return;
+    }
     Blk cur = load_block<ALIGNED>(p);
     for (uint64_t b = 0; b < nb; b++) {
         uint32_t w[16];
