@@ -2,11 +2,12 @@
 //   copy      : 1 read : 1 write streaming copy (the guide's 6.3 TB/s reference pattern)
 //   stream12  : the RS access pattern with no arithmetic -- 4 x 16-B reads, 8 x 16-B writes per
 //               lane per 16 positions (each output = xor of the inputs), same grid and strides
-//   rs        : rs_code_kernel<4> as shipped (256-entry x 8-B LDS table per input, one lookup per
+//   rs_byte   : round 1's rs_code_kernel (256-entry x 8-B LDS table per input, one lookup per
 //               input byte, bank conflicts from random indices)
-//   rs_nib    : nibble tables, 32 bank-pair replicas (conflict-free ds_read_b64, 2 lookups/byte)
+//   rs        : rs_code_kernel<4> as shipped: nibble tables, 32 bank-pair replicas
+//               (conflict-free ds_read_b64, 2 lookups per byte)
 // Data: 256 segments x 32 MiB (8 GiB in, 16 GiB out), GF(2^8) tables from random coefficients.
-// rs_nib is checked byte for byte against rs.  Build: hipcc --offload-arch=gfx950 -O3 tools/rs_ab.hip
+// The shipped kernel is checked byte for byte against round 1's.  Build: hipcc --offload-arch=gfx950 -O3 tools/rs_ab.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -103,15 +104,13 @@ __global__ __launch_bounds__(256) void stream12_kernel(dm::RsArgs a) {
     }
 }
 
-// Nibble tables: entry e in 0..15 = T[e] (low nibble), 16..31 = T[e << 4] (high nibble); replica
-// c = lane & 31 of entry e at uint2 index e * 32 + c, so a lane always reads banks 2c, 2c+1.
-constexpr int kNib = 32;
+// Round-1 form of rs_code_kernel: one 256-entry x 8-B table per input, one lookup per byte
+// (random indices: 68 % of LDS cycles were bank conflicts).
 template <int NIN>
-__global__ __launch_bounds__(256) void rs_nib_kernel(dm::RsArgs a, const uint2* __restrict__ nib) {
-    __shared__ uint2 tab[NIN * kNib * 32];
-    for (uint32_t t = threadIdx.x; t < NIN * kNib * 32; t += 256) tab[t] = nib[t / 32];
+__global__ __launch_bounds__(256) void rs_byte_kernel(dm::RsArgs a) {
+    __shared__ uint2 tab[NIN * 256];
+    for (uint32_t t = threadIdx.x; t < NIN * 256; t += 256) tab[t] = a.table[t];
     __syncthreads();
-    const uint32_t rep = threadIdx.x & 31;
     const uint64_t ustride = (uint64_t)gridDim.x * 256;
     for (uint64_t seg = blockIdx.y; seg < a.nseg; seg += gridDim.y) {
         const uint64_t ib = seg * a.in_seg_stride, ob = seg * a.out_seg_stride;
@@ -136,15 +135,14 @@ __global__ __launch_bounds__(256) void rs_nib_kernel(dm::RsArgs a, const uint2* 
 #pragma unroll
             for (int j = 0; j < NIN; j++) {
                 const uint32_t w[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-                const uint2* tj = tab + j * kNib * 32 + rep;
+                const uint2* tj = tab + j * 256;
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t lo = (w[q] >> (8 * k)) & 15u, hi = (w[q] >> (8 * k + 4)) & 15u;
-                        const uint2 e0 = tj[lo * 32], e1 = tj[(16 + hi) * 32];
-                        acc[4 * q + k].x ^= e0.x ^ e1.x;
-                        acc[4 * q + k].y ^= e0.y ^ e1.y;
+                        const uint2 e = tj[(w[q] >> (8 * k)) & 0xffu];
+                        acc[4 * q + k].x ^= e.x;
+                        acc[4 * q + k].y ^= e.y;
                     }
                 }
             }
@@ -164,6 +162,8 @@ __global__ __launch_bounds__(256) void rs_nib_kernel(dm::RsArgs a, const uint2* 
         }
     }
 }
+
+constexpr int kNib = dm::kRsNibEntries;
 
 int main() {
     const int K = 4, M = 8;
@@ -202,7 +202,7 @@ int main() {
     CK(hipMalloc(&dnib, nib.size() * 8));
     CK(hipMemcpy(dtab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(dnib, nib.data(), nib.size() * 8, hipMemcpyHostToDevice));
-    auto args = [&](uint8_t* out) {
+    auto args = [&](uint8_t* out, const uint2* table) {
         dm::RsArgs a{};
         for (int j = 0; j < K; j++) a.in[j] = din + j * shard;
         for (int i = 0; i < M; i++) a.out[i] = out + i * shard;
@@ -210,7 +210,7 @@ int main() {
         a.out_seg_stride = M * shard;
         a.units_per_seg = shard / 16;
         a.nseg = nseg;
-        a.table = dtab;
+        a.table = table;
         a.nout = M;
         return a;
     };
@@ -245,28 +245,28 @@ int main() {
         hipLaunchKernelGGL(copy_kernel, dim3(8 * cus), dim3(256), 0, 0, (const uint4*)din, (uint4*)dout, in_bytes / 16);
     });
     timeit("stream12u<1, plain stores>", rs_bytes, [&] {
-        hipLaunchKernelGGL((stream12u_kernel<1, false>), dim3(gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL((stream12u_kernel<1, false>), dim3(gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
     timeit("stream12u<2, nt stores>", rs_bytes, [&] {
-        hipLaunchKernelGGL((stream12u_kernel<2, true>), dim3(gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL((stream12u_kernel<2, true>), dim3(gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
     timeit("stream12u<2, plain stores>", rs_bytes, [&] {
-        hipLaunchKernelGGL((stream12u_kernel<2, false>), dim3(gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL((stream12u_kernel<2, false>), dim3(gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
     timeit("stream12u<1, nt>, 2x grid", rs_bytes, [&] {
-        hipLaunchKernelGGL((stream12u_kernel<1, true>), dim3(2 * gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL((stream12u_kernel<1, true>), dim3(2 * gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
     timeit("stream12u<1, nt>, 4x grid", rs_bytes, [&] {
-        hipLaunchKernelGGL((stream12u_kernel<1, true>), dim3(4 * gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL((stream12u_kernel<1, true>), dim3(4 * gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
     timeit("stream12 (RS pattern, no tables)", rs_bytes, [&] {
-        hipLaunchKernelGGL(stream12_kernel, dim3(gx, gy), dim3(256), 0, 0, args(dout));
+        hipLaunchKernelGGL(stream12_kernel, dim3(gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
-    timeit("rs_code_kernel<4> (shipped)", rs_bytes, [&] {
-        hipLaunchKernelGGL(dm::rs_code_kernel<4>, dim3(gx, gy), dim3(256), 0, 0, args(dout));
+    timeit("rs_byte_kernel<4> (round 1: 256-entry tables)", rs_bytes, [&] {
+        hipLaunchKernelGGL(rs_byte_kernel<4>, dim3(gx, gy), dim3(256), 0, 0, args(dout, dtab));
     });
-    timeit("rs_nib_kernel<4> (conflict-free nibble tables)", rs_bytes, [&] {
-        hipLaunchKernelGGL(rs_nib_kernel<4>, dim3(gx, gy), dim3(256), 0, 0, args(dout2), (const uint2*)dnib);
+    timeit("rs_code_kernel<4> (shipped: replicated nibble tables)", rs_bytes, [&] {
+        hipLaunchKernelGGL(dm::rs_code_kernel<4>, dim3(gx, gy), dim3(256), 0, 0, args(dout2, dnib));
     });
     CK(hipDeviceSynchronize());
     std::vector<uint8_t> a(64 << 20), b(64 << 20);
@@ -276,6 +276,6 @@ int main() {
         CK(hipMemcpy(b.data(), dout2 + o, b.size(), hipMemcpyDeviceToHost));
         same = std::memcmp(a.data(), b.data(), a.size()) == 0;
     }
-    std::printf("{\"rs_nib_equals_rs\": %s}\n", same ? "true" : "false");
+    std::printf("{\"shipped_equals_round1\": %s}\n", same ? "true" : "false");
     return same ? 0 : 2;
 }
