@@ -81,6 +81,9 @@ def main() -> None:
     ap.add_argument("--e2e", action="store_true", help="also time the host-buffer path (N=1)")
     ap.add_argument("--no-e2e", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N=1 object line: skip the other configs / entry points measured in the same run "
+                         "(other_configs), the e2e host-buffer rates and the 64 KiB / 1 MiB sweep points")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--workload", default="object",
                     choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files",
@@ -132,22 +135,16 @@ def main() -> None:
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
 
-    if args.workload == "upload":
-        return run_upload(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "files":
-        return run_files(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "plumbing":
-        return run_plumbing(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "rs":
-        return run_rs(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "process":
-        return run_process(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "proofs":
-        return run_proofs(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload == "concurrent":
-        return run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo)
-    if args.workload != "object":
-        return run_batch(args, torch, dist, world, rank, device, dev_index, gloo)
+    runners = {"upload": run_upload, "files": run_files, "plumbing": run_plumbing, "rs": run_rs,
+               "process": run_process, "proofs": run_proofs, "concurrent": run_concurrent,
+               "batch": run_batch, "stream": run_batch}
+    if args.workload in runners:
+        res = runners[args.workload](args, torch, dist, world, rank, device, dev_index, gloo)
+        if res is not None and rank == 0:
+            print(json.dumps(res), flush=True)
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+        return
     chunk = args.chunk
     total = int(args.total_gib * (1 << 30)) if args.total_gib else int(args.object_gib * (1 << 30)) * world
     plan = plan_shards(total, chunk, world)
@@ -291,11 +288,68 @@ def main() -> None:
             out["vs_baseline"] = round(value / cpu, 4)
             out["vs_baseline_basis"] = (f"GPU value / the {out['parity']['cpu_threads']}-thread CPU restatement "
                                         "over the same synthetic object (regenerated leaf by leaf), same run")
+    if world == 1 and rank == 0 and not args.no_extras:
+        del buf
+        torch.cuda.empty_cache()
+        out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+def _summary(r):
+    """The fields of a workload's result line worth keeping inside the headline line."""
+    if not isinstance(r, dict):
+        return {"error": "no result"}
+    keep = {k: r[k] for k in ("metric", "value", "unit", "ms_per_step", "steps") if k in r}
+    keep["workload"] = r.get("config", {}).get("workload")
+    par = r.get("parity", {})
+    keep["bit_exact"] = par.get("bit_exact")
+    for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel"):
+        if k in r:
+            keep[k] = r[k]
+    if "leaf_kernel" in r.get("config", {}):
+        keep["leaf_kernel"] = r["config"]["leaf_kernel"]
+    rf = r.get("roofline")
+    if rf:
+        keep["roofline"] = {k: rf.get(k) for k in ("kernel", "achieved", "peak", "unit", "frac", "traffic")}
+    if "cpu_baseline" in r:
+        keep["cpu_baseline"] = r["cpu_baseline"]
+    return keep
+
+
+def driver_extras(args, torch, dist, device, dev_index):
+    """N = 1 only: the other BASELINE configs and entry points, measured in the same run as the
+    headline so the round's driver records them (each is also its own --workload).  A failing
+    extra is reported as an error field; it never fails the headline."""
+    import copy
+    specs = [
+        ("configs[2]", run_batch, dict(workload="batch", objects=4096, object_mib=4.0, steps=3, warmup=1)),
+        ("configs[4]_per_gpu_share", run_batch, dict(workload="stream", objects=12500, object_mib=1.0, steps=2,
+                                                     warmup=1)),
+        ("files_NewHashTree", run_files, dict(workload="files", objects=256, object_mib=32.0, steps=2, warmup=1,
+                                              no_cpu=True)),
+        ("upload_stream_1MiB_chunks", run_upload, dict(workload="upload", chunk=1 << 20, object_gib=8.0, steps=2,
+                                                       warmup=1)),
+        ("FullProcessing", run_process, dict(workload="process", object_gib=8.0, steps=2, warmup=1, no_cpu=True)),
+        ("reed_solomon_4+8", run_rs, dict(workload="rs", object_gib=8.0, steps=3, warmup=1, no_cpu=True)),
+    ]
+    res = {}
+    for name, fn, kw in specs:
+        ns = copy.copy(args)
+        ns.__dict__.update(kw)
+        t0 = time.perf_counter()
+        try:
+            r = _summary(fn(ns, torch, dist, 1, 0, device, dev_index, False))
+        except Exception as e:   # reported, never fatal to the headline line
+            r = {"error": f"{type(e).__name__}: {e}"}
+        r["wall_s"] = round(time.perf_counter() - t0, 2)
+        res[name] = r
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    return res
 
 
 def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, chunk, root_hex, barrier, gloo):
@@ -435,7 +489,7 @@ def run_files(args, torch, dist, world, rank, device, dev_index, gloo):
                                    "kind": "port", "sample": f"{len(sample)} of the same files: read whole (io.ReadAll), "
                                    "then serial SHA-256 leaves + tree (oracle/merkle_oracle.c, SHA-NI)"}
             del chunks
-        print(json.dumps(out), flush=True)
+        return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -480,7 +534,7 @@ def run_plumbing(args, torch, dist, world, rank, device, dev_index, gloo):
         "parity": {"fixture_root": case["root"], "cpu_root": cpu_root.hex(), "gpu_root": gpu_root,
                    "bit_exact": cpu_root.hex() == case["root"] == gpu_root},
     }
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
@@ -530,7 +584,7 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         "write_ms": round((tavg - sum(tails) / len(tails)) * 1e3, 3),
         "parity": {"root": root.hex(), "cpu_root": want.hex(), "bit_exact": root == want},
     }
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def load_rs_traffic(key: str):
@@ -642,7 +696,7 @@ def run_rs(args, torch, dist, world, rank, device, dev_index, gloo):
                                "sample": f"{sample} segments x {seg} B of the same data, scalar table-driven "
                                          "GF(2^8) encode (oracle/rs_oracle.c, stands in for klauspost's Go path)",
                                "parallel": {"value": round(res[max(res)], 4), "cores": max(res)}}
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def timed_steps(args, torch, dist, world, device, gloo, ctx, step):
@@ -754,7 +808,7 @@ def run_process(args, torch, dist, world, rank, device, dev_index, gloo):
         out["cpu_baseline"] = {"value": round(sample * seg / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
                                "kind": "port", "sample": f"{sample} segments x {seg} B of the same object through "
                                "oracle/process_oracle.c (SHA-NI SHA-256 + table GF(2^8) RS, serial like the SDK)"}
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
@@ -816,7 +870,7 @@ def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
         "content_GiBps": round(n * leaf * world * args.steps / elapsed / (1 << 30), 3),
         "parity": {"all_proofs_verify": all_ok, "root_matches_cpu": root_ok, "bit_exact": all_ok and root_ok},
     }
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo):
@@ -933,7 +987,7 @@ def run_concurrent(args, torch, dist, world, rank, device, dev_index, gloo):
                                  "note": "one dm_ctx for all threads: calls serialise (timed on a sample of "
                                          "256 (root) / 8 (process) requests, scaled)"}
         out["speedup_vs_shared_context"] = round(res["shared_context"] / res["batcher"], 2)
-    print(json.dumps(out), flush=True)
+    return out
 
 
 def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
@@ -1045,11 +1099,9 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
         dist.all_reduce(t)
         out["parity"] = {"checked_objects": int(t[1]), "mismatches": int(t[0]), "bit_exact": int(t[0]) == 0,
                          "ranks": world}
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
-        dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
@@ -1058,7 +1110,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     from oracle import Oracle   # CPU baseline / checker only
     orc = Oracle()
     host = None
-    do_e2e = args.e2e and not args.no_e2e
+    do_e2e = (args.e2e or not args.no_extras) and not args.no_e2e
     if not args.no_cpu or do_e2e:
         host = torch.empty(length, dtype=torch.uint8, pin_memory=True)
         host.copy_(buf[:length])
@@ -1096,6 +1148,9 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
                       "root_matches": r.hex() == root_hex and r2.hex() == root_hex,
                       "path": "host buffer -> (pinned ring | direct) H2D, striped, overlapped with the leaf "
                               "kernel -> tree -> 32 B root back (dm_root_buffer)"}
+    if not args.sweep and not args.no_extras and not args.no_sweep:
+        # the GPU / host crossover: 1 MiB and 64 KiB chunks of the same object
+        args.sweep, args.sweep_chunks = True, "65536,1048576"
     if args.sweep and not args.no_sweep:
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)

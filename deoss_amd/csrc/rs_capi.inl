@@ -66,19 +66,15 @@ bool gf_invert(const uint8_t* m, int k, uint8_t* out) {
     return true;
 }
 
-// Nibble tables of `rows` (nout x k, row-major) for rs_code_kernel: input j, entry e < 16 holds
-// the products of the low nibble x = e, entry 16 + e those of the high nibble x = e << 4; byte i
-// of an entry = rows[i][j] * x.  GF(2^8) multiplication is xor-linear, so the lookups of a byte's
-// two nibbles xor to its full product.
+// Lookup table of `rows` (nout x k, row-major): entry [j][x] byte i = rows[i][j] * x.
 std::vector<uint64_t> rs_table(const uint8_t* rows, int nout, int k) {
     const Gf& g = gf();
-    std::vector<uint64_t> t((size_t)k * dm::kRsNibEntries, 0);
+    std::vector<uint64_t> t((size_t)k * 256, 0);
     for (int j = 0; j < k; j++)
-        for (int e = 0; e < dm::kRsNibEntries; e++) {
-            const uint8_t x = (uint8_t)(e < 16 ? e : (e - 16) << 4);
-            uint64_t v = 0;
-            for (int i = 0; i < nout; i++) v |= (uint64_t)g.mul(rows[i * k + j], x) << (8 * i);
-            t[(size_t)j * dm::kRsNibEntries + e] = v;
+        for (int x = 0; x < 256; x++) {
+            uint64_t e = 0;
+            for (int i = 0; i < nout; i++) e |= (uint64_t)g.mul(rows[i * k + j], (uint8_t)x) << (8 * i);
+            t[(size_t)j * 256 + x] = e;
         }
     return t;
 }
@@ -89,7 +85,7 @@ struct dm_rs {
     dm_ctx* c = nullptr;
     int k = 0, m = 0;
     std::vector<uint8_t> mat;   // (k + m) x k
-    DevBuf enc_tab;             // parity rows, k x 32 nibble entries x 8 B
+    DevBuf enc_tab;             // parity rows, k x 256 x 8 B
     DevBuf dec_tab;             // per reconstruct call
     DevBuf work;                // host-API shard staging
 };

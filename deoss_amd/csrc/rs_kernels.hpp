@@ -7,17 +7,17 @@
 // (polynomial 0x11d), M = Vandermonde x inverse(top square).  The same kernel applies any
 // (nout x nin) GF matrix, so Reconstruct uses it with a decode matrix built on the host.
 //
-// HBM-bound byte work, not a GEMM: an input byte x of shard j contributes T_j[x] = (M[0][j]*x, ...,
-// M[7][j]*x) -- 8 bytes, its products for all (up to 8) outputs at the same position -- and the
-// contributions of the nin inputs are xor-ed.  GF(2^8) products are xor-linear in x, so T_j[x] =
-// T_j[x & 15] ^ T_j[x & 0xf0]: two lookups in 16-entry nibble tables per byte.  Each table lives
-// in LDS as 32 replicas interleaved so that lane l reads only banks 2(l%32), 2(l%32)+1: every
-// ds_read_b64 is conflict-free whatever the data (a 256-entry table read by random bytes spent 68 %
-// of its LDS cycles on bank conflicts).  Measured (tools/rs_ab.hip, profiles/r02/r02c_rs_ab.log):
-// 5.19 TB/s vs 5.05 for the 256-entry form and 5.05 for the same access pattern with no lookups.
+// HBM-bound byte work, not a GEMM: every input byte x of shard j is looked up ONCE in an LDS
+// table T_j[x] whose 8 bytes are (M[0][j]*x, ..., M[7][j]*x) -- the contributions of that byte to
+// all (up to 8) outputs at the same position -- and the lookups of the nin inputs are xor-ed.
 // A lane owns 16 consecutive positions (one uint4 per shard), so per 16 positions it issues nin
-// 16-B loads, 32*nin ds_read_b64, and nout 16-B stores; the position-major accumulators are
+// 16-B loads, 16*nin ds_read_b64, and nout 16-B stores; the position-major accumulators are
 // turned into shard-major output words by 4x4 byte transposes (v_perm_b32).
+// What bounds it (tools/rs_ab.hip, profiles/r02/r02d_rs_ab_repeats.log, interleaved repeats on one
+// box): this kernel 5.09 ms per 8 GiB of segments, the same access pattern with no table at all
+// 5.13 ms, a conflict-free variant (replicated nibble tables, 0 bank conflicts) 5.23 ms.  The
+// random-index bank conflicts (68 % of LDS cycles) are hidden under the 1-read : 2-write HBM
+// stream, which itself runs at 5.0 TB/s against 6.2-6.3 TB/s for a 1:1 copy.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,8 +27,6 @@ namespace dm {
 constexpr int kRsMaxIn = 8;
 constexpr int kRsMaxOut = 8;
 constexpr int kRsThreads = 256;
-constexpr int kRsNibEntries = 32;   // per input: 16 low-nibble + 16 high-nibble entries
-constexpr int kRsReplicas = 32;     // one replica per bank pair of a ds_read_b64 lane group
 
 struct RsArgs {
     const uint8_t* in[kRsMaxIn];   // input shard j of segment 0
@@ -37,7 +35,7 @@ struct RsArgs {
     uint64_t out_seg_stride;       // bytes from segment s to s+1 (outputs)
     uint64_t units_per_seg;        // shard bytes / 16
     uint64_t nseg;
-    const uint2* table;            // [nin][32] x 8 B nibble tables (rs_capi.inl rs_table)
+    const uint2* table;            // [nin][256] x 8 B: byte i of entry x = M[i][j] * x
     uint32_t nout;
 };
 
@@ -90,11 +88,9 @@ __global__ __launch_bounds__(kRsThreads)
 __attribute__((amdgpu_waves_per_eu(DM_RS_WAVES)))
 #endif
 void rs_code_kernel(RsArgs a) {
-    // entry e of input j, replica r at [(j * 32 + e) * 32 + r]
-    __shared__ uint2 tab[NIN * kRsNibEntries * kRsReplicas];
-    for (uint32_t t = threadIdx.x; t < NIN * kRsNibEntries * kRsReplicas; t += kRsThreads) tab[t] = a.table[t / kRsReplicas];
+    __shared__ uint2 tab[NIN * 256];
+    for (uint32_t t = threadIdx.x; t < NIN * 256; t += kRsThreads) tab[t] = a.table[t];
     __syncthreads();
-    const uint32_t rep = threadIdx.x % kRsReplicas;
     const uint64_t ustride = (uint64_t)gridDim.x * kRsThreads;
     for (uint64_t seg = blockIdx.y; seg < a.nseg; seg += gridDim.y) {
         const uint64_t ib = seg * a.in_seg_stride;
@@ -121,15 +117,14 @@ void rs_code_kernel(RsArgs a) {
 #pragma unroll
             for (int j = 0; j < NIN; j++) {
                 const uint32_t w[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-                const uint2* tj = tab + j * kRsNibEntries * kRsReplicas + rep;
+                const uint2* tj = tab + j * 256;
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
 #pragma unroll
                     for (int k = 0; k < 4; k++) {
-                        const uint32_t lo = (w[q] >> (8 * k)) & 15u, hi = (w[q] >> (8 * k + 4)) & 15u;
-                        const uint2 e0 = tj[lo * kRsReplicas], e1 = tj[(16 + hi) * kRsReplicas];
-                        acc[4 * q + k].x ^= e0.x ^ e1.x;
-                        acc[4 * q + k].y ^= e0.y ^ e1.y;
+                        const uint2 e = tj[(w[q] >> (8 * k)) & 0xffu];
+                        acc[4 * q + k].x ^= e.x;
+                        acc[4 * q + k].y ^= e.y;
                     }
                 }
             }
