@@ -73,6 +73,10 @@ def main() -> None:
     ap.add_argument("--total-gib", type=float, default=0.0,
                     help="object bytes across all ranks (GiB); 1024 at --gpus 8 = BASELINE configs[3] "
                          "(1 TiB, 128 GiB per rank); 0 = --object-gib per GPU")
+    ap.add_argument("--multi-configs", action="store_true",
+                    help="rehearsal: run the 8-GPU extras (configs[3], configs[4]) at any N > 1")
+    ap.add_argument("--cfg3-total-gib", type=float, default=1024.0, help=argparse.SUPPRESS)
+    ap.add_argument("--cfg4-objects", type=int, default=100000, help=argparse.SUPPRESS)
     ap.add_argument("--prefix-gib", type=float, default=64.0,
                     help="N>1 parity: sharded root vs single-GPU root of a prefix of at most this size")
     ap.add_argument("--chunk", type=int, default=32 << 20, help="chunk (leaf) bytes; default 32 MiB")
@@ -145,6 +149,36 @@ def main() -> None:
         if world > 1 and dist.is_initialized():
             dist.destroy_process_group()
         return
+    def barrier():
+        if world > 1:
+            if gloo:
+                torch.cuda.synchronize()
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[dev_index])
+        torch.cuda.synchronize()
+
+    out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
+    if world == 1 and rank == 0 and not args.no_extras:
+        out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
+    if ((world == 8 and not args.same_device) or (world > 1 and args.multi_configs)) and not args.no_extras \
+            and not args.total_gib:
+        other = multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
+        if rank == 0:
+            out["other_configs"] = other
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        barrier()
+        dist.destroy_process_group()
+
+
+def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
+    """One object over all ranks (BASELINE configs[1] at N = 1, the weak-scaling curve, configs[3]
+    with --total-gib 1024): timed steps, roofline, parity legs.  Returns rank 0's line (other ranks
+    get theirs too, unused).  Buffers are released before returning."""
+    from deoss_amd import MerkleContext, plan_shards
+    from deoss_amd.sharding import sharded_root
     chunk = args.chunk
     total = int(args.total_gib * (1 << 30)) if args.total_gib else int(args.object_gib * (1 << 30)) * world
     plan = plan_shards(total, chunk, world)
@@ -173,15 +207,6 @@ def main() -> None:
         else:
             sharded_root(plan, rank, subtree, finish, torch, dist, device,
                          comm_device="cpu" if gloo else None)
-
-    def barrier():
-        if world > 1:
-            if gloo:
-                torch.cuda.synchronize()
-                dist.barrier()
-            else:
-                dist.barrier(device_ids=[dev_index])
-        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -288,15 +313,43 @@ def main() -> None:
             out["vs_baseline"] = round(value / cpu, 4)
             out["vs_baseline_basis"] = (f"GPU value / the {out['parity']['cpu_threads']}-thread CPU restatement "
                                         "over the same synthetic object (regenerated leaf by leaf), same run")
-    if world == 1 and rank == 0 and not args.no_extras:
-        del buf
-        torch.cuda.empty_cache()
-        out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        barrier()
-        dist.destroy_process_group()
+    del ctx
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+
+def multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
+    """N = 8: BASELINE configs[3] (one 1 TiB object, 128 GiB and 4,096 leaves per GPU, sharded
+    root + both parity legs) and configs[4] (100,000 x 1 MiB objects from pinned host memory,
+    12,500 per GPU, replicas), measured in the same run as the weak-scaling line so the driver's
+    8-GPU run records them.  Every rank takes part in both (collectives); configs[3] runs only if
+    every rank has the HBM for it, agreed by one all-reduce before anything is allocated."""
+    import copy
+    res = {}
+    need = int(args.cfg3_total_gib * (1 << 30)) // world + (8 << 30)
+    free, _ = torch.cuda.mem_get_info(device)
+    ok = torch.tensor([1 if free >= need else 0], dtype=torch.int64, device="cpu" if gloo else device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    t0 = time.perf_counter()
+    if int(ok.item()):
+        ns = copy.copy(args)
+        ns.total_gib, ns.steps, ns.warmup, ns.no_extras = args.cfg3_total_gib, 3, 1, True
+        r = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
+        res["configs[3]"] = _summary(r)
+    else:
+        res["configs[3]"] = {"skipped": f"a rank has less than {need} B of free HBM"}
+    res["configs[3]"]["wall_s"] = round(time.perf_counter() - t0, 2)
+    barrier()
+    t0 = time.perf_counter()
+    ns = copy.copy(args)
+    ns.workload, ns.total_objects, ns.object_mib, ns.steps, ns.warmup = "stream", args.cfg4_objects, 1.0, 2, 1
+    res["configs[4]"] = _summary(run_batch(ns, torch, dist, world, rank, device, dev_index, gloo))
+    res["configs[4]"]["wall_s"] = round(time.perf_counter() - t0, 2)
+    torch.cuda.empty_cache()
+    barrier()
+    return res
 
 
 def _summary(r):
@@ -307,6 +360,11 @@ def _summary(r):
     keep["workload"] = r.get("config", {}).get("workload")
     par = r.get("parity", {})
     keep["bit_exact"] = par.get("bit_exact")
+    if "prefix_bit_exact" in par or "ranks" in par:
+        keep["parity"] = par
+    for k in ("n_gpus", "scaling"):
+        if k in r:
+            keep[k] = r[k]
     for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel"):
         if k in r:
             keep[k] = r[k]

@@ -96,7 +96,7 @@ def _prefix_worker(rank, world, port, cases, results):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_multi_rank_parity_plan_gloo(world):
     cases = [(1 << 20, 4096, 11, 1 << 20),          # prefix = whole object
              (1 << 20, 4096, 12, 300 * 1024),       # prefix shorter than the object (the 1 TiB case)
