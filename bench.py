@@ -365,7 +365,7 @@ def _summary(r):
     for k in ("n_gpus", "scaling"):
         if k in r:
             keep[k] = r[k]
-    for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel"):
+    for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel", "cpu", "gpu"):
         if k in r:
             keep[k] = r[k]
     if "leaf_kernel" in r.get("config", {}):
@@ -384,6 +384,7 @@ def driver_extras(args, torch, dist, device, dev_index):
     extra is reported as an error field; it never fails the headline."""
     import copy
     specs = [
+        ("configs[0]", run_plumbing, dict(workload="plumbing", steps=2, warmup=1)),
         ("configs[2]", run_batch, dict(workload="batch", objects=4096, object_mib=4.0, steps=3, warmup=1)),
         ("configs[4]_per_gpu_share", run_batch, dict(workload="stream", objects=12500, object_mib=1.0, steps=2,
                                                      warmup=1)),

@@ -16,9 +16,9 @@ from cess-go-sdk (``go.mod:8``; not vendored): ``node/objectHandler.go:168``,
   them by path and match ``filepath.Base`` against a requested hash, ``node/fileHandler.go:967-969``);
 * the fid is the hex ``common/hashtree`` root over the segments.
 
-Coding, hashing and the tree run on the GPU; there is no CPU fallback.  Deviations:
-the segment files themselves are not written (their bytes are the data fragments in order), and
-a non-empty ``cipher`` is rejected (the AES branch is not implemented).
+Coding, hashing and the tree run on the GPU; there is no CPU fallback.  Segment files are written
+too (the zero-padded segment = its data fragments in order), so every returned path exists.
+Deviation: a non-empty ``cipher`` is rejected (the AES branch is not implemented).
 """
 from __future__ import annotations
 
@@ -157,7 +157,11 @@ class Processor:
                                 with open(path, "wb") as out:
                                     out.write(frags[t * self.frag:(t + 1) * self.frag])
                             names.append(path)
-                        info.append(SegmentDataInfo(os.path.join(savedir, segd[32 * s:32 * s + 32].hex()), names))
+                        seg_path = os.path.join(savedir, segd[32 * s:32 * s + 32].hex())
+                        if not os.path.exists(seg_path):   # data fragments in order = the padded segment
+                            with open(seg_path, "wb") as out:
+                                out.write(frags[s * total * self.frag:(s * total + self.k) * self.frag])
+                        info.append(SegmentDataInfo(seg_path, names))
                     if len(buf) < window:
                         break
         except (OSError, DeossMerkleError) as e:

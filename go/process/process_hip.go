@@ -12,8 +12,9 @@
 // segments in flight, DEOSS_PROCESS_MEM_GIB (default 8) windows at once across every upload,
 // buffers pooled, fragments written to disk as each window completes.  Swap it in by changing the handlers' import of
 // github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
-// Deviations: cipher must be "" (the AES branch is not implemented), and segment files are not
-// written (their bytes are the data fragments in order).  Build with `-tags hip`, CGO_ENABLED=1.
+// Deviation: cipher must be "" (the AES branch is not implemented; INTEGRATION.md).  Segment and
+// fragment files are both written to savedir under their hex SHA-256.  Build with `-tags hip`,
+// CGO_ENABLED=1.
 package process
 
 /*
@@ -51,6 +52,9 @@ var (
 	initEr  error
 	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
 	bufs    sync.Pool     // *windowBuf, reused across calls
+	// writeSegments: SegmentHash paths exist as files (the zero-padded segment bytes), like the
+	// fragment paths; DEOSS_SKIP_SEGMENT_FILES=1 skips them (DeOSS itself only opens fragments).
+	writeSegments = os.Getenv("DEOSS_SKIP_SEGMENT_FILES") != "1"
 )
 
 type windowBuf struct {
@@ -139,6 +143,20 @@ func runWindow(f *os.File, w *window, savedir string) {
 		p := filepath.Join(savedir, hex.EncodeToString(b.fragd[32*t:32*t+32]))
 		if _, err := os.Stat(p); err != nil {
 			if err = os.WriteFile(p, b.frags[t*frag:(t+1)*frag], os.ModePerm); err != nil {
+				w.err = err
+				return
+			}
+		}
+	}
+	if !writeSegments {
+		return
+	}
+	// SegmentHash names a file too: the zero-padded segment, i.e. its data fragments in order
+	for s := uint64(0); s < w.nseg; s++ {
+		p := filepath.Join(savedir, hex.EncodeToString(b.segd[32*s:32*s+32]))
+		if _, err := os.Stat(p); err != nil {
+			first := s * total * frag
+			if err = os.WriteFile(p, b.frags[first:first+seg], os.ModePerm); err != nil {
 				w.err = err
 				return
 			}

@@ -117,6 +117,8 @@ def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch):
     assert len(info) == 11
     for s, si in enumerate(info):
         assert os.path.basename(si.SegmentHash) == seg_b[32 * s:32 * s + 32].hex()
+        padded = data[s * 4096:(s + 1) * 4096]
+        assert open(si.SegmentHash, "rb").read() == padded + bytes(4096 - len(padded))
         assert len(si.FragmentHash) == 12
         for j, path in enumerate(si.FragmentHash):
             t = s * 12 + j
