@@ -349,6 +349,33 @@ def test_new_hash_tree_files_layouts(ctx, oracle_lib, tmp_path, sharded, leaf_mo
             c.close()
 
 
+def test_new_hash_tree_special_files(ctx, oracle_lib, tmp_path):
+    """One file; one empty file (root = H(H('') || H(''))); a FIFO read to EOF like io.ReadAll
+    (non-regular files are read whole at open time)."""
+    p = tmp_path / "one"
+    p.write_bytes(b"content_one")
+    leaves, root = ctx.new_hash_tree([str(p)])
+    assert root == oracle_lib.root_chunks([b"content_one"])[1]
+    e = tmp_path / "empty"
+    e.write_bytes(b"")
+    leaves, root = ctx.new_hash_tree([str(e)])
+    h0 = hashlib.sha256(b"").digest()
+    assert leaves == [h0] and root == hashlib.sha256(h0 + h0).digest()
+    fifo = tmp_path / "fifo"
+    os.mkfifo(fifo)
+    body = oracle_lib.splitmix_bytes(300_000, 77)
+
+    def writer():
+        with open(fifo, "wb") as f:
+            for i in range(0, len(body), 4096):
+                f.write(body[i:i + 4096])
+    t = threading.Thread(target=writer)
+    t.start()
+    leaves, root = ctx.new_hash_tree([str(p), str(fifo), str(e)])
+    t.join()
+    assert root == oracle_lib.root_chunks([b"content_one", body, b""])[1]
+
+
 def test_new_hash_tree_go_errors(ctx, tmp_path):
     """types.go:24-33 reads files in order and returns the first failure, with Go's text."""
     from deoss_amd import DeossMerkleError
