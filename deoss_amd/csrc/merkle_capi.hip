@@ -424,11 +424,24 @@ int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uin
     // Pinned sources (every chunk in page-locked host memory): async copies straight from the
     // caller's buffers, coalescing runs that are contiguous on both sides with no padding between
     // them (so a copy never reads a host byte outside the caller's chunks).
+    // One runtime query per pinned allocation, not per chunk: chunks inside the range of the last
+    // pinned allocation found need no query (12,500 queries cost ~30 ms per call).
     bool all_pinned = true;
+    uintptr_t lo = 0, hi = 0;
     for (uint64_t i = 0; i < n && all_pinned; i++) {
         if (lens[i] == 0) continue;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(ptrs[i]);
+        if (p >= lo && p + lens[i] <= hi) continue;
         hipPointerAttribute_t attr{};
         all_pinned = hipPointerGetAttributes(&attr, ptrs[i]) == hipSuccess && attr.type == hipMemoryTypeHost;
+        void* start = nullptr;
+        size_t size = 0;
+        if (all_pinned &&
+            hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)ptrs[i]) == hipSuccess &&
+            hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)ptrs[i]) == hipSuccess) {
+            lo = reinterpret_cast<uintptr_t>(start);
+            hi = lo + size;
+        }
     }
     (void)hipGetLastError();
     if (all_pinned) {
@@ -1011,8 +1024,12 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
-    for (uint64_t o = 0; o < nobj; o++)
+    uint64_t bytes = 0;
+    for (uint64_t o = 0; o < nobj; o++) {
         if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
+        if (!objs[o]) return fail(c, DM_ERR_INVALID, "object %llu: NULL pointer", (unsigned long long)o);
+        bytes += lens[o];
+    }
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));
     std::vector<uint64_t> addr;

@@ -181,6 +181,32 @@ def test_batch_ragged_objects(ctx, oracle_lib, leaf_mode):
     assert [got[32 * i:32 * i + 32] for i in range(len(objs))] == wants
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+def test_batch_pipelined_host(ctx, oracle_lib, pinned):
+    """dm_root_batch over > 256 MiB of host objects: groups copied while earlier groups hash
+    (root_batch_pipelined), ragged sizes and multi-leaf objects, pinned and pageable sources."""
+    torch = _torch()
+    import random
+    rnd = random.Random(23)
+    lens = [rnd.choice([1, 4095, 1 << 20, (1 << 20) + 7, 3 << 20, 200000]) for _ in range(400)]
+    pitch = [(n + 4095) // 4096 * 4096 for n in lens]
+    offs = [sum(pitch[:i]) for i in range(len(lens))]
+    host = torch.empty(sum(pitch), dtype=torch.uint8, pin_memory=pinned)
+    for i, n in enumerate(lens):
+        oracle_lib.fill_splitmix_ptr(host.data_ptr() + offs[i], 0, (n + 7) // 8 * 8, 5000 + i)   # pitch >= that
+    import ctypes as ct
+    n = len(lens)
+    P = (ct.c_void_p * n)(*[host.data_ptr() + o for o in offs])
+    L = (ct.c_uint64 * n)(*lens)
+    out = ct.create_string_buffer(32 * n)
+    assert sum(lens) > (256 << 20)
+    ctx._check(ctx._L.dm_root_batch(ctx._h, P, L, n, 1 << 20, out), "dm_root_batch")
+    got = out.raw
+    for i in range(n):
+        want = oracle_lib.root_buffer_ptr(host.data_ptr() + offs[i], lens[i], 1 << 20)[1]
+        assert got[32 * i:32 * i + 32] == want, i
+
+
 def test_batch_misaligned_device_objects(ctx, oracle_lib, leaf_mode):
     """Table mode over device objects starting at 1..15-byte offsets (unaligned loads through
     global-address-space pointers taken from the table)."""
