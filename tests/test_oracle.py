@@ -161,3 +161,41 @@ def test_root_synthetic_matches_buffer(oracle_lib):
         oracle_lib.root_synthetic(0, 64, 1)
     with pytest.raises(ValueError):
         oracle_lib.root_synthetic(64, 100, 1)
+
+
+# ---- property tests (hypothesis): the C restatement == the hashlib restatement == the literal
+# merkletree v0.2.0 recursion on arbitrary chunk lists, and sharded composition == whole root
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+_chunk_lists = st.lists(st.binary(min_size=0, max_size=300), min_size=1, max_size=70)
+
+
+@settings(max_examples=120, deadline=None)
+@given(_chunk_lists)
+def test_property_c_oracle_equals_python_and_go_recursion(oracle_lib, chunks):
+    leaves, root = py_root_chunks(chunks)
+    assert oracle_lib.root_chunks(chunks, nthreads=2) == (b"".join(leaves), root)
+    go_leafs, go_root = py_go_tree(chunks)
+    assert go_root == root
+    assert len(go_leafs) == len(chunks) + len(chunks) % 2      # merkletree's duplicated last leaf
+
+
+@settings(max_examples=120, deadline=None)
+@given(st.integers(min_value=1, max_value=3000), st.integers(min_value=1, max_value=9),
+       st.integers(min_value=0, max_value=2 ** 32))
+def test_property_sharded_levels_compose(n, world, seed):
+    """For any leaf count and rank count, per-rank k-level subtrees concatenated and finished
+    give the whole-object root (the multi-GPU plan)."""
+    from deoss_amd.sharding import plan_shards
+    rnd = random.Random(seed)
+    digests = [rnd.getrandbits(256).to_bytes(32, "big") for _ in range(n)]
+    plan = plan_shards(n * 64, 64, world)
+    nodes = []
+    for r in range(world):
+        l0, l1 = plan.leaf_range(r)
+        if l1 > l0:
+            part = py_reduce(digests[l0:l1], plan.k) if plan.k else digests[l0:l1]
+            assert len(part) == plan.node_count(r)
+            nodes.extend(part)
+    finished = py_reduce(nodes) if (plan.k == 0 or len(nodes) > 1) else nodes
+    assert finished[0] == py_reduce(digests)[0]
