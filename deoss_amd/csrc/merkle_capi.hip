@@ -1024,11 +1024,9 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
     std::lock_guard<std::mutex> lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
-    uint64_t bytes = 0;
     for (uint64_t o = 0; o < nobj; o++) {
         if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
         if (!objs[o]) return fail(c, DM_ERR_INVALID, "object %llu: NULL pointer", (unsigned long long)o);
-        bytes += lens[o];
     }
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));

@@ -381,6 +381,9 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_lat(LeafArgs a) {
     // trip count shared by both waves (each computes the same maximum over the 64 leaves)
     const uint64_t NB = wave_max_u64(v.nb);
     if (producer) {
+        // One block (half a 128-B line) per iteration.  Loading whole lines here, as K1 does, took
+        // the traffic at 64 KiB chunks from 1.047x to 1.000x but cost 3 % there and 6 % at 512 KiB
+        // chunks (16,384 leaves, where K1L is chosen): profiles/r02/k1l_lines_ab/summary.log.
         Blk cur;
         if (v.nb > 0) cur = load_block<ALIGNED>(v.p);
         for (uint64_t b = 0; b < NB; b++) {

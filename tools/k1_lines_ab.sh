@@ -7,7 +7,7 @@ set -e
 out=$1; shift
 mkdir -p $out
 export TMPDIR=/tmp
-args="--no-cpu --chunk 65536 --leaf-kernel wide --sweep --sweep-chunks 4096,65536 --sweep-modes --steps 3 --warmup 1"
+args=${ARGS:-"--no-cpu --chunk 65536 --leaf-kernel wide --sweep --sweep-chunks 4096,65536 --sweep-modes --steps 3 --warmup 1"}
 for v in "$@"; do
   lib=$PWD/build_variants/$v.so
   DEOSS_MERKLE_LIB=$lib timeout -k 10 120 python bench.py $args > $out/$v.bench.json
