@@ -4,7 +4,7 @@
 leaf kernel (16-B aligned variants: the bench path), finds its per-block loop in the gfx950
 assembly and counts the instructions of one 64-byte block:
 
-* ``wide`` (K1, one lane per leaf): the loop streaming 4 x global_load_dwordx4 per block;
+* ``wide`` (K1, one lane per leaf): the loop streaming 8 x global_load_dwordx4 per two blocks;
 * ``latency`` (K1L) and ``pair`` (K1P): the consumer loop (16 ds_read_b128 of K+W per block)
   and the producer loop (16 ds_write_b128 per block);
 * ``quad`` (K1Q): the consumer's whole-stage loop (8 blocks from registers, 128 ds_read_b128)
@@ -97,11 +97,15 @@ def _smallest(loops, pred):
 
 
 def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
-    """Per-block counts of the wide kernel's streaming loop."""
-    loops = list(_loops(_function_body(asm, sym)))
-    lp = _smallest(loops, lambda l: sum(x.startswith("global_load_dwordx4") for x in l) >= 4)
-    if lp is None:
+    """Per-block counts of the wide kernel's streaming loop.  K1 absorbs two blocks (one 128-B
+    line, eight 16-B loads) per iteration, and the second block sits behind a leaf-end branch that
+    jumps to the latch, so the iteration is the LARGEST backward-branch region holding the loads
+    (the smaller one ends at that branch and holds only the first block's rounds)."""
+    loops = [l for l in _loops(_function_body(asm, sym))
+             if sum(x.startswith("global_load_dwordx4") for x in l) >= 4]
+    if not loops:
         raise ValueError("no block loop found")
+    lp = max(loops, key=len)
     loads = sum(x.startswith("global_load_dwordx4") for x in lp)
     return _summary(lp, max(1, loads // 4))
 
