@@ -6,11 +6,13 @@
 //   MerkleTree{Leafs, MerkleRoot()}                  cbergoon/merkletree v0.2.0 (go.mod:10)
 // Leafs has n entries, n+1 when n is odd (last leaf duplicated, dup = true), as merkletree's
 // buildWithContent makes it.  Interior nodes are not materialised (the GPU reduces the tree).
-// Header-only; link with -ldeoss_merkle.
+// Also the Go package's additions: Init / DEOSS_GPUS (every GPU by default), NewHashTreeFromBuffer
+// and the hash-while-receiving Stream.  Header-only; link with -ldeoss_merkle.
 #pragma once
 
 #include <array>
 #include <cstdint>
+#include <cstdlib>
 #include <memory>
 #include <optional>
 #include <string>
@@ -51,7 +53,35 @@ struct MerkleTree {
     const Digest& MerkleRoot() const { return Root.Hash; }
 };
 
-// Process-wide GPU context (device 0), created on first use.
+// GPUs of the process-wide context, as the Go package chooses them (go/hashtree/types_hip.go):
+// Init(devs) before first use, else DEOSS_GPUS ("0,1,2,3" or "all"), else every visible GPU.
+// With more than one, NewHashTree / NewHashTreeFromBuffer shard by aligned chunk ranges.
+inline std::vector<int>& selected_devices() {
+    static std::vector<int> devs;
+    return devs;
+}
+
+inline std::vector<int> device_list() {
+    if (!selected_devices().empty()) return selected_devices();
+    std::vector<int> out;
+    const char* env = std::getenv("DEOSS_GPUS");
+    std::string spec = env ? env : "";
+    if (!spec.empty() && spec != "all") {
+        size_t pos = 0;
+        while (pos <= spec.size()) {
+            const size_t comma = spec.find(',', pos);
+            const std::string f = spec.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+            if (!f.empty()) out.push_back(std::atoi(f.c_str()));
+            if (comma == std::string::npos) break;
+            pos = comma + 1;
+        }
+        return out;
+    }
+    for (int i = 0; i < dm_gpu_count(); i++) out.push_back(i);
+    return out;
+}
+
+// Process-wide GPU context, created on first use.
 class Context {
   public:
     static Context& instance() {
@@ -65,14 +95,25 @@ class Context {
     }
 
   private:
-    Context() { rc_ = dm_create(&ctx_, nullptr, 0); }
+    Context() {
+        const std::vector<int> devs = device_list();
+        rc_ = devs.empty() ? DM_ERR_NODEV : dm_create(&ctx_, devs.data(), (int)devs.size());
+    }
     dm_ctx* ctx_ = nullptr;
     int rc_ = DM_OK;
 };
 
+// Init(devs) of the Go package: must run before the first call that creates the context.
+inline std::optional<Error> Init(const std::vector<int>& devs) {
+    if (devs.empty()) return Error{DM_ERR_INVALID, "hashtree: Init needs at least one device"};
+    selected_devices() = devs;
+    return std::nullopt;
+}
+
+// dm_last_error is the calling thread's message: read it right after the failing call.
 inline Error make_error(dm_ctx* c, int rc) {
     if (rc == DM_ERR_EMPTY) return {rc, "Empty data"};
-    std::string m = c ? dm_last_error(c) : "";
+    std::string m = dm_last_error(c);
     return {rc, m.empty() ? std::string(dm_strerror(rc)) : m};
 }
 
@@ -112,16 +153,74 @@ inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTree(
 
 // Additive: one in-memory object split into chunkSize chunks (the upload-handler buffer).
 inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTreeFromBuffer(
-    const void* buf, uint64_t len, uint64_t chunkSize) {
+    const void* buf, uint64_t len, int64_t chunkSize) {
+    if (chunkSize <= 0) return {nullptr, Error{DM_ERR_INVALID, "hashtree: chunk size must be positive"}};
     if (len == 0) return {nullptr, Error{DM_ERR_EMPTY, "Empty data"}};
     Context& cx = Context::instance();
     if (cx.status() != DM_OK) return {nullptr, Error{cx.status(), dm_strerror(cx.status())}};
-    const uint64_t n = chunkSize ? (len + chunkSize - 1) / chunkSize : 0;
+    const uint64_t n = (len + (uint64_t)chunkSize - 1) / (uint64_t)chunkSize;
     std::vector<uint8_t> leaves(32 * n);
     Digest root{};
-    int rc = dm_root_buffer(cx.get(), buf, len, chunkSize, leaves.data(), root.data());
+    int rc = dm_root_buffer(cx.get(), buf, len, (uint64_t)chunkSize, leaves.data(), root.data());
     if (rc != DM_OK) return {nullptr, make_error(cx.get(), rc)};
     return {build(leaves, root), std::nullopt};
 }
+
+// Hash-while-receiving, as the Go Stream (go/hashtree/stream_hip.go): Write pieces of any size,
+// Close() returns the tree NewHashTreeFromBuffer builds over the concatenated bytes, Abort()
+// drops it.  One thread at a time per Stream.
+class Stream {
+  public:
+    static std::pair<std::unique_ptr<Stream>, std::optional<Error>> New(int64_t chunkSize) {
+        if (chunkSize <= 0 || chunkSize % 16)
+            return {nullptr, Error{DM_ERR_INVALID, "hashtree: stream chunk size must be a positive multiple of 16"}};
+        Context& cx = Context::instance();
+        if (cx.status() != DM_OK) return {nullptr, Error{cx.status(), dm_strerror(cx.status())}};
+        std::unique_ptr<Stream> s(new Stream((uint64_t)chunkSize));
+        const int rc = dm_stream_open(cx.get(), (uint64_t)chunkSize, &s->st_);
+        if (rc != DM_OK) return {nullptr, make_error(cx.get(), rc)};
+        return {std::move(s), std::nullopt};
+    }
+    std::optional<Error> Write(const void* p, uint64_t len) {
+        if (!st_) return Error{DM_ERR_INVALID, "hashtree: write on a closed stream"};
+        if (err_) return err_;
+        if (len == 0) return std::nullopt;
+        const int rc = dm_stream_write(st_, p, len);
+        if (rc != DM_OK) {
+            err_ = make_error(Context::instance().get(), rc);
+            return err_;
+        }
+        received_ += len;
+        return std::nullopt;
+    }
+    std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> Close() {
+        if (!st_) return {nullptr, Error{DM_ERR_INVALID, "hashtree: stream already closed"}};
+        dm_stream* st = st_;
+        st_ = nullptr;
+        if (err_) {
+            dm_stream_abort(st);
+            return {nullptr, err_};
+        }
+        const uint64_t n = (received_ + chunk_ - 1) / chunk_;
+        std::vector<uint8_t> leaves(32 * (n ? n : 1));
+        Digest root{};
+        uint64_t got = 0;
+        const int rc = dm_stream_close(st, leaves.data(), n, &got, root.data());
+        if (rc != DM_OK) return {nullptr, make_error(Context::instance().get(), rc)};
+        leaves.resize(32 * n);
+        return {build(leaves, root), std::nullopt};
+    }
+    void Abort() {
+        if (st_) dm_stream_abort(st_);
+        st_ = nullptr;
+    }
+    ~Stream() { Abort(); }
+
+  private:
+    explicit Stream(uint64_t chunk) : chunk_(chunk) {}
+    dm_stream* st_ = nullptr;
+    uint64_t chunk_ = 0, received_ = 0;
+    std::optional<Error> err_;
+};
 
 }  // namespace hashtree

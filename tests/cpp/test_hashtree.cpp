@@ -2,6 +2,7 @@
 // API (include/deoss_hashtree.hpp) and the GPU library.  Prints "PASS" and exits 0 on success.
 // Expected digests are computed independently with the CPU oracle's SHA-256 (linked in only as
 // the checker, never by the product library).
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -67,6 +68,40 @@ int main(int argc, char** argv) {
     std::string obj = "content_onecontent_two";
     auto [tb, eb] = hashtree::NewHashTreeFromBuffer(obj.data(), obj.size(), 11);
     EXPECT(!eb && tb && tb->MerkleRoot() == sha(cat(hashes[0], hashes[1])));
+
+    auto [tz, ez] = hashtree::NewHashTreeFromBuffer(obj.data(), obj.size(), 0);
+    EXPECT(!tz && ez && ez->code == DM_ERR_INVALID);
+
+    // Stream: the Go NewStream call sequence (pieces of any size, Close, Abort, empty body)
+    std::string body;
+    for (int i = 0; i < 300000; i++) body.push_back((char)(i * 131 + (i >> 9)));
+    auto [whole, ew] = hashtree::NewHashTreeFromBuffer(body.data(), body.size(), 4096);
+    EXPECT(!ew && whole);
+    auto [st, es] = hashtree::Stream::New(4096);
+    EXPECT(!es && st);
+    for (size_t pos = 0, step = 1; st && pos < body.size(); step = step * 7 % 100003 + 1) {
+        const size_t m = std::min(step, body.size() - pos);
+        EXPECT(!st->Write(body.data() + pos, m));
+        pos += m;
+    }
+    if (st) {
+        auto [ts, ec] = st->Close();
+        EXPECT(!ec && ts && whole && ts->MerkleRoot() == whole->MerkleRoot() && ts->Leafs.size() == whole->Leafs.size());
+        auto [tc2, ec2] = st->Close();
+        EXPECT(!tc2 && ec2);
+    }
+    auto [se, ese] = hashtree::Stream::New(64);
+    if (se) {
+        auto [te, ee] = se->Close();
+        EXPECT(!te && ee && ee->message == "Empty data");
+    }
+    auto [sa, esa] = hashtree::Stream::New(64);
+    if (sa) {
+        EXPECT(!sa->Write(body.data(), 1000));
+        sa->Abort();
+    }
+    auto [sb, esb] = hashtree::Stream::New(100);
+    EXPECT(!sb && esb && esb->code == DM_ERR_INVALID);
 
     if (fails) return 1;
     std::printf("PASS\n");
