@@ -6,6 +6,7 @@ The compute path is ``libdeoss_merkle.so`` (hand-written HIP for gfx950, C ABI i
 from ._lib import DeossMerkleError, LIB_PATH, load_library  # noqa: F401
 from .merkle import MerkleContext  # noqa: F401
 from .hashtree import (  # noqa: F401
-    HashTreeContent, MerkleTree, NewHashTree, NewHashTreeFromBuffer, NewHashTreesBatch, Node,
+    HashTreeContent, Init, MerkleTree, NewHashTree, NewHashTreeFromBuffer, NewHashTreesBatch, NewStream, Node,
+    Stream,
 )
 from .sharding import ShardPlan, plan_shards  # noqa: F401

@@ -29,12 +29,36 @@ from ._lib import DeossMerkleError
 from .merkle import MerkleContext
 
 _default_ctx: Optional[MerkleContext] = None
+_selected: Optional[List[int]] = None
+
+
+def Init(devs: Sequence[int]) -> Optional[Exception]:
+    """The Go package's Init(devs): the GPUs the default context spans (before first use)."""
+    global _selected
+    if _default_ctx is not None:
+        return DeossMerkleError(-2, "hashtree: Init after first use")
+    if not devs:
+        return DeossMerkleError(-2, "hashtree: Init needs at least one device")
+    _selected = list(devs)
+    return None
+
+
+def _device_list() -> List[int]:
+    """Init(devs), else DEOSS_GPUS ("0,1,2,3" or "all"), else every visible GPU."""
+    import os
+    from ._lib import load_library
+    if _selected:
+        return _selected
+    spec = os.environ.get("DEOSS_GPUS", "").strip()
+    if spec and spec != "all":
+        return [int(x) for x in spec.split(",") if x.strip()]
+    return list(range(load_library().dm_gpu_count())) or [0]
 
 
 def default_context() -> MerkleContext:
     global _default_ctx
     if _default_ctx is None:
-        _default_ctx = MerkleContext()
+        _default_ctx = MerkleContext(devices=_device_list())
     return _default_ctx
 
 
@@ -181,6 +205,8 @@ def NewHashTree(chunkPath: Sequence[str], ctx: Optional[MerkleContext] = None,
 def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContext] = None
                           ) -> Tuple[Optional[MerkleTree], Optional[Exception]]:
     """Additive: the object buffer split into chunkSize chunks (last one short)."""
+    if chunkSize <= 0:
+        return None, DeossMerkleError(-2, f"hashtree: chunk size {chunkSize} must be positive")
     if len(buf) == 0:
         return None, DeossMerkleError(-1, "Empty data")
     c = ctx or default_context()
@@ -198,5 +224,57 @@ def NewHashTreesBatch(objects: Sequence[bytes], chunkSize: int, ctx: Optional[Me
     c = ctx or default_context()
     try:
         return c.root_batch(list(objects), chunkSize), None
+    except DeossMerkleError as e:
+        return None, e
+
+
+class Stream:
+    """The Go package's hash-while-receiving Stream (go/hashtree/stream_hip.go) over dm_stream:
+    ``Write(piece)`` any number of times, ``Close()`` -> ``(tree, err)`` equal to
+    NewHashTreeFromBuffer over the concatenated bytes, ``Abort()``."""
+
+    def __init__(self, st, chunk: int):
+        self._st, self._chunk, self._received, self._err = st, chunk, 0, None
+
+    def Write(self, p: bytes) -> Tuple[int, Optional[Exception]]:
+        if self._st is None:
+            return 0, DeossMerkleError(-2, "hashtree: write on a closed stream")
+        if self._err is not None:
+            return 0, self._err
+        try:
+            self._st.write(p)
+        except DeossMerkleError as e:
+            self._err = e
+            return 0, e
+        self._received += len(p)
+        return len(p), None
+
+    def Close(self) -> Tuple[Optional["MerkleTree"], Optional[Exception]]:
+        if self._st is None:
+            return None, DeossMerkleError(-2, "hashtree: stream already closed")
+        st, self._st = self._st, None
+        if self._err is not None:
+            st.abort()
+            return None, self._err
+        n = -(-self._received // self._chunk)
+        try:
+            leaves, root = st.close(want_leaves=True, leaf_cap=n)
+        except DeossMerkleError as e:
+            return None, e
+        return _build(leaves, root, [None] * n, st._ctx), None
+
+    def Abort(self) -> None:
+        if self._st is not None:
+            self._st.abort()
+            self._st = None
+
+
+def NewStream(chunkSize: int, ctx: Optional[MerkleContext] = None) -> Tuple[Optional[Stream], Optional[Exception]]:
+    """NewStream(chunkSize): chunkSize a positive multiple of 16 (DeOSS: chain.SegmentSize)."""
+    if chunkSize <= 0 or chunkSize % 16:
+        return None, DeossMerkleError(-2, f"hashtree: stream chunk size {chunkSize} must be a positive multiple of 16")
+    c = ctx or default_context()
+    try:
+        return Stream(c.open_stream(chunkSize), chunkSize), None
     except DeossMerkleError as e:
         return None, e

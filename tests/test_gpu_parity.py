@@ -68,6 +68,31 @@ def test_new_hash_tree_reference_kat(tmp_path):
     assert roothashs.hex() == "b513419286835c1e36fa520b86cbf37650db82e73f510f0e6a699cc0505f1151"
 
 
+def test_go_stream_mirror():
+    """NewStream / Write / Close / Abort as the Go package exposes them (go/hashtree/stream_hip.go)."""
+    from deoss_amd import Init, NewHashTreeFromBuffer, NewStream
+    body = bytes((i * 131 + (i >> 9)) & 0xff for i in range(300000))
+    whole, err = NewHashTreeFromBuffer(body, 4096)
+    assert err is None
+    st, err = NewStream(4096)
+    assert err is None
+    pos, step = 0, 1
+    while pos < len(body):
+        m = min(step, len(body) - pos)
+        assert st.Write(body[pos:pos + m]) == (m, None)
+        pos, step = pos + m, step * 7 % 100003 + 1
+    tree, err = st.Close()
+    assert err is None and tree.MerkleRoot() == whole.MerkleRoot() and len(tree.Leafs) == len(whole.Leafs)
+    assert st.Close()[1] is not None
+    empty, _ = NewStream(64)
+    assert str(empty.Close()[1]) == "Empty data"
+    ab, _ = NewStream(64)
+    ab.Write(body[:1000])
+    ab.Abort()
+    assert NewStream(100)[1] is not None and NewHashTreeFromBuffer(body, 0)[1] is not None
+    assert Init([0]) is not None      # the default context already exists: Init after first use
+
+
 def test_new_hash_tree_errors_and_dup(tmp_path):
     from deoss_amd import NewHashTree
     tree, err = NewHashTree([])
