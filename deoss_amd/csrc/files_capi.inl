@@ -13,6 +13,7 @@
 //    resumable leaf launch of step j, so every leaf chain is in flight from the first stripe and the
 //    call ends one stripe after the last read instead of one leaf-chain after it.
 #include <fcntl.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -39,7 +40,12 @@ struct FileSet {
 // types.go:24-33: files are opened and read in order and the first failure is returned, with Go's
 // messages: "open <path>: <errno text>", "read <path>: is a directory".
 int open_files(dm_ctx* c, const char* const* paths, uint64_t n, FileSet& fs) {
-    const bool keep_open = n <= 256;   // stay well inside the default 1,024-descriptor limit
+    // Keep every file open when the descriptor limit allows (Go raises the soft limit to the hard
+    // one at start-up; Python keeps 1,024): striped reads touch every file once per step, and
+    // reopening 4,096 files per step would cost more than reading them.
+    struct rlimit rl {};
+    const uint64_t limit = getrlimit(RLIMIT_NOFILE, &rl) == 0 ? (uint64_t)rl.rlim_cur : 1024;
+    const bool keep_open = n + 256 <= limit;
     fs.path.resize(n);
     fs.size.assign(n, 0);
     fs.fd.assign(n, -1);
