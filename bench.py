@@ -23,6 +23,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0            # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_SLOT_PEAK = 256 * 128 * 2.4e9   # 256 CU x 4 SIMD-32 x 2.4 GHz: full-rate int32 lane-slots/s
+MAX_CLOCK_HZ = 2.4e9                  # MI355X_MICROARCH.md chip parameters
+ISSUE_CYCLES_ONE_WAVE = 4             # one wave alone issues a VALU instruction every 4 cycles (same guide)
 SEED = 0xDE0550002               # configs[1] seed (0xDE0550000 + k)
 
 
@@ -293,6 +295,17 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         },
         "root": root_hex,
     }
+    if kind != "wide" and vpb and k1_avg_ms:
+        # The bound that applies to few long leaves: one leaf's serial chain on its consumer wave,
+        # which issues at most one VALU instruction every 4 cycles (MI355X_MICROARCH.md, "vector-
+        # instruction ISSUE cost, one wave's stream on one SIMD") at the 2.4 GHz maximum clock.
+        blocks_per_leaf = (chunk + 9 + 63) // 64
+        floor_ms = blocks_per_leaf * vpb * ISSUE_CYCLES_ONE_WAVE / MAX_CLOCK_HZ * 1e3
+        out["roofline"]["chain_issue_floor"] = {
+            "valu_per_block_on_chain": vpb, "cycles_per_valu_one_wave": ISSUE_CYCLES_ONE_WAVE,
+            "clock_ghz": MAX_CLOCK_HZ / 1e9, "blocks_per_leaf": blocks_per_leaf, "floor_ms": round(floor_ms, 3),
+            "frac": round(floor_ms / k1_avg_ms, 4),
+            "note": "time of one leaf chain at one issue per 4 cycles: the latency-bound kernel's roofline"}
 
     if args.same_device:
         out["ranks"] = world
