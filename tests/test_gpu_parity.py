@@ -287,6 +287,46 @@ def test_many_leaves_multi_stage(ctx, oracle_lib, leaf_mode):
     assert got == want
 
 
+@pytest.fixture(scope="module")
+def big_leaves(ctx, oracle_lib):
+    """Two leaves longer than 512 MiB, so the 64-bit FIPS 180-4 length word has a non-zero high
+    half: leaf 0 ends 61 bytes into its last block (length in a second padding block), leaf 1
+    ends 5 bytes in (length in the same block)."""
+    torch = _torch()
+    chunk = (1 << 29) + 61
+    length = chunk + (1 << 29) + 5
+    buf = torch.empty(length + 64, dtype=torch.uint8, device="cuda")
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, (length + 7) // 8 * 8, 0x5A, torch.cuda.current_stream().cuda_stream)
+    host = ctypes.create_string_buffer((length + 7) // 8 * 8)
+    oracle_lib.fill_splitmix_ptr(ctypes.addressof(host), 0, (length + 7) // 8 * 8, 0x5A)
+    leaves, want = oracle_lib.root_buffer_ptr(ctypes.addressof(host), length, chunk, 2, True)
+    del host
+    torch.cuda.synchronize()
+    yield buf, length, chunk, leaves, want
+    del buf
+    torch.cuda.empty_cache()
+
+
+def test_leaf_length_above_512MiB(ctx, big_leaves, leaf_mode):
+    buf, length, chunk, want_leaves, want = big_leaves
+    assert (chunk * 8) >> 32 == 1
+    got, lv = root_dev(ctx, buf.data_ptr(), length, chunk, want_leaves=True)
+    assert lv == want_leaves
+    assert got == want
+    if leaf_mode != "quad":
+        return   # K1 / K1L / K1P chains take 15-22 s per 512 MiB leaf: table mode checked under K1Q
+    # table mode (batch): each leaf as its own one-leaf object, the second one misaligned
+    torch = _torch()
+    roots = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    ctx.root_batch_device_async([buf.data_ptr(), buf.data_ptr() + chunk], [chunk, length - chunk], 1 << 31,
+                                roots.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    r = bytes(roots.cpu().numpy())
+    for k in range(2):
+        h = want_leaves[32 * k:32 * k + 32]
+        assert r[32 * k:32 * k + 32] == hashlib.sha256(h + h).digest(), k
+
+
 def test_empty_and_invalid(ctx):
     from deoss_amd import DeossMerkleError
     with pytest.raises(DeossMerkleError, match="Empty data"):
