@@ -31,6 +31,7 @@ import (
 // Stream hashes one object whose bytes arrive in pieces of any size.  It is used by one goroutine
 // at a time; many streams may be open at once (they share the package's GPU context).
 type Stream struct {
+	c        *C.dm_ctx
 	st       *C.dm_stream
 	chunk    uint64
 	received uint64
@@ -47,7 +48,7 @@ func NewStream(chunkSize int) (*Stream, error) {
 	if err != nil {
 		return nil, err
 	}
-	s := &Stream{chunk: uint64(chunkSize)}
+	s := &Stream{c: c, chunk: uint64(chunkSize)}
 	runtime.LockOSThread()
 	defer runtime.UnlockOSThread()
 	if rc := C.dm_stream_open(c, C.uint64_t(chunkSize), &s.st); rc != C.DM_OK {
@@ -72,7 +73,7 @@ func (s *Stream) Write(p []byte) (int, error) {
 	runtime.LockOSThread()
 	defer runtime.UnlockOSThread()
 	if rc := C.dm_stream_write(s.st, unsafe.Pointer(&p[0]), C.uint64_t(len(p))); rc != C.DM_OK {
-		s.err = rcError(ctx, rc)
+		s.err = rcError(s.c, rc)
 		return 0, s.err
 	}
 	s.received += uint64(len(p))
@@ -101,7 +102,7 @@ func (s *Stream) Close() (*merkletree.MerkleTree, error) {
 	rc := C.dm_stream_close(st, (*C.uint8_t)(unsafe.Pointer(&leaves[0])), C.uint64_t(n), &got,
 		(*C.uint8_t)(unsafe.Pointer(&root[0])))
 	if rc != C.DM_OK {
-		return nil, rcError(ctx, rc)
+		return nil, rcError(s.c, rc)
 	}
 	if uint64(got) != n {
 		return nil, fmt.Errorf("hashtree: stream closed with %d leaves, expected %d", uint64(got), n)
