@@ -253,7 +253,7 @@ extern "C" {
 
 int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t* leaf_out, uint8_t root[32]) {
     if (!ctx || !root || (n && !paths)) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");   // types.go:20-22
     FileSet fs;

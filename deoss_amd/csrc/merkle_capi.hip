@@ -173,6 +173,30 @@ int fail(dm_ctx* c, int code, const char* fmt, ...) {
 // which is also what torch's default stream handle (0) denotes.
 hipStream_t pick_stream(Dev&, void* s) { return static_cast<hipStream_t>(s); }
 
+// Every entry point leaves the calling thread's current HIP device as it found it: the library
+// switches devices per call, and a caller's own device (torch's, a Go thread's) must not move.
+struct DeviceRestore {
+    int prev = -1;
+    DeviceRestore() {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+            (void)hipGetLastError();
+        }
+    }
+    ~DeviceRestore() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceRestore(const DeviceRestore&) = delete;
+    DeviceRestore& operator=(const DeviceRestore&) = delete;
+};
+
+// An entry point's hold on its context: the context lock, and the caller's device restored after.
+struct CallLock {
+    DeviceRestore dev;
+    std::lock_guard<std::mutex> lk;
+    explicit CallLock(std::mutex& m) : lk(m) {}
+};
+
 // Order this call's use of the context scratch after the previous call's (possibly other stream).
 int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
     HIP_TRY(hipSetDevice(d.id));
@@ -812,6 +836,7 @@ int dm_gpu_count(void) {
 int dm_create(dm_ctx** out, const int* devs, int ndev) {
     if (!out) return bad_arg();
     *out = nullptr;
+    DeviceRestore dev;
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return set_err(DM_ERR_NODEV, "no usable GPU");
     std::vector<int> ids;
@@ -848,6 +873,7 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
 
 void dm_destroy(dm_ctx* ctx) {
     if (!ctx) return;
+    DeviceRestore dev;
     for (auto& cm : ctx->comms) (void)ncclCommDestroy(cm);
     for (auto& d : ctx->devs) destroy_device(d);
     delete ctx;
@@ -855,20 +881,20 @@ void dm_destroy(dm_ctx* ctx) {
 
 int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
     if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_QUAD) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     ctx->leaf_mode = mode;
     return DM_OK;
 }
 
 int dm_leaf_kernel_for(dm_ctx* ctx, uint64_t nleaves) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     return pick_leaf_kernel(ctx, ctx->devs[0], nleaves);
 }
 
 int dm_set_timing(dm_ctx* ctx, int enable) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     ctx->timing = enable != 0;
     for (auto& d : ctx->devs) d.ntimed = 0;
     return DM_OK;
@@ -876,7 +902,7 @@ int dm_set_timing(dm_ctx* ctx, int enable) {
 
 int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double* total_ms_sum, double* leaf_ms_max) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     uint64_t n = 0;
     double a = 0, b = 0, mx = 0;
@@ -904,7 +930,7 @@ int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double
 int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, void* dev_root,
                          void* leaf_out_dev, void* stream) {
     if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     Dev& d = ctx->devs[0];
     return root_device_impl(ctx, d, pick_stream(d, stream), dev, len, chunk, static_cast<uint8_t*>(dev_root),
                             static_cast<uint8_t*>(leaf_out_dev));
@@ -912,7 +938,7 @@ int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t ch
 
 int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!dev && len)) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     Dev& d = c->devs[0];
     RC_TRY(root_device_impl(c, d, d.stream, dev, len, chunk, d.root.u8(), nullptr));
@@ -924,7 +950,7 @@ int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, u
 int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint32_t levels,
                             void* dev_nodes, uint64_t* n_out, void* stream) {
     if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[0];
@@ -941,7 +967,7 @@ int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t
 int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int min_one_level, void* dev_root,
                            void* stream) {
     if (!ctx || !dev_nodes || !dev_root) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[0];
@@ -954,7 +980,7 @@ int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int m
 int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const uint64_t* lens, uint64_t nobj,
                                uint64_t chunk, void* dev_roots, void* stream) {
     if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
     Dev& d = c->devs[0];
@@ -965,7 +991,7 @@ int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const u
 
 int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbytes, uint64_t seed, void* stream) {
     if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nbytes == 0) return DM_OK;
     Dev& d = c->devs[0];
@@ -981,7 +1007,7 @@ int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbyte
 
 int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!host && len)) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if ((c->devs.size() > 1 || c->force_sharded) && ceil_div(len, chunk) >= 2 * c->devs.size())
@@ -995,7 +1021,7 @@ int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, 
 int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out,
                    uint8_t root[32]) {
     if (!ctx || !root || (n && (!ptrs || !lens))) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     for (uint64_t i = 0; i < n; i++)
@@ -1021,7 +1047,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
 int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
                   uint8_t* roots) {
     if (!ctx || chunk == 0 || (nobj && (!objs || !lens || !roots))) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
     for (uint64_t o = 0; o < nobj; o++) {

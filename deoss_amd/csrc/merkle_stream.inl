@@ -188,8 +188,9 @@ extern "C" {
 int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     if (!ctx || !out || chunk == 0) return bad_arg();
     *out = nullptr;
+    DeviceRestore dev;
     if (chunk % 16 != 0) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        CallLock lk(ctx->mu);
         return fail(ctx, DM_ERR_INVALID, "dm_stream: chunk must be a multiple of 16 bytes");
     }
     dm_stream* st = new dm_stream();
@@ -223,7 +224,7 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
         }
     } while (0);
     if (rc != DM_OK) {
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        CallLock lk(ctx->mu);
         ctx->err = st->err;
         t_err = st->err;
         stream_free(st);
@@ -235,6 +236,7 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
 
 int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
     if (!st || (!data && len)) return bad_arg();
+    DeviceRestore dev;
     SHIP(hipSetDevice(st->c->devs[st->dev].id));
     const uint8_t* p = static_cast<const uint8_t*>(data);
     while (len) {
@@ -260,6 +262,7 @@ const char* dm_stream_error(dm_stream* st) { return st ? st->err.c_str() : ""; }
 
 int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_t* nleaves, uint8_t root[32]) {
     if (!st || !root) return bad_arg();
+    DeviceRestore dev;
     dm_ctx* c = st->c;
     int rc = DM_OK;
     t_err.clear();
@@ -275,7 +278,7 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         if ((rc = stream_launch(st, n, st->received - (n - 1) * st->chunk)) != DM_OK) break;
         if (nleaves) *nleaves = n;
         // tree over all leaf digests on the context's stream, after every compute stream
-        std::lock_guard<std::mutex> lk(c->mu);
+        CallLock lk(c->mu);
         Dev& d = c->devs[st->dev];
         hipStream_t s = d.stream;
         if ((rc = begin_call(c, d, s)) != DM_OK) break;
@@ -303,7 +306,7 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         if ((e = hipStreamSynchronize(s)) != hipSuccess) rc = fail(c, DM_ERR_HIP, "close sync: %s", hipGetErrorString(e));
     } while (0);
     if (rc != DM_OK && !st->err.empty()) {
-        std::lock_guard<std::mutex> lk(c->mu);
+        CallLock lk(c->mu);
         if (c->err.empty() || rc == DM_ERR_EMPTY) c->err = st->err;
         if (t_err.empty() || rc == DM_ERR_EMPTY) t_err = st->err;
     }
@@ -311,6 +314,9 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
     return rc;
 }
 
-void dm_stream_abort(dm_stream* st) { stream_free(st); }
+void dm_stream_abort(dm_stream* st) {
+    DeviceRestore dev;
+    stream_free(st);
+}
 
 }  // extern "C"

@@ -116,7 +116,7 @@ uint32_t dm_tree_depth(uint64_t n) { return tree_depth(n); }
 
 int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n, void* dev_nodes, void* stream) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (!aligned_all({dev_leaves, dev_nodes}))
@@ -129,7 +129,7 @@ int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n,
 
 int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t* nodes_out) {
     if (!ctx || (n && (!leaf_digests || !nodes_out))) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[0];
@@ -148,7 +148,7 @@ int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t
 int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void* dev_nodes, uint64_t n,
                                  const void* dev_idx, uint64_t q, void* dev_paths, void* dev_bits, void* stream) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
@@ -166,7 +166,7 @@ int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void
 int dm_merkle_paths(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, const uint64_t* idx, uint64_t q,
                     uint8_t* paths, uint8_t* bits) {
     if (!ctx || (n && !leaf_digests) || (q && (!idx || !paths || !bits))) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
@@ -195,7 +195,7 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
                                  const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                  uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     if (!dev_contents || !lens || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
@@ -216,7 +216,7 @@ int dm_verify_object_device_async(dm_ctx* ctx, const void* dev_obj, uint64_t len
                                   const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                   uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (chunk == 0 || !dev_obj || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
@@ -235,7 +235,7 @@ int dm_verify_paths(dm_ctx* ctx, const void* const* contents, const uint64_t* le
     if (!ctx || (q && (!contents || !lens || !paths || !bits || !roots || !ok)) || depth == 0 ||
         (root_stride != 0 && root_stride != 32))
         return bad_arg();
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     for (uint64_t t = 0; t < q; t++)

@@ -18,6 +18,8 @@
  *    for odd n is NOT written (it equals leaf n-1).
  *  - Ownership: the caller owns every buffer; nothing is retained after return.
  *  - Threading: a context serialises its calls internally; separate contexts run in parallel.
+ *  - Every call leaves the calling thread's current HIP device as it found it (the library
+ *    switches to its context's devices inside the call and switches back).
  *  - `stream` arguments are hipStream_t values passed as void*, used verbatim (NULL is HIP's
  *    null stream, e.g. torch's default stream).  *_async calls only enqueue work on that
  *    stream; device inputs must be ready in stream order and outputs are valid once the
