@@ -237,7 +237,7 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
     k1_bytes = local_len + 32 * ((local_len + chunk - 1) // chunk)   # read N once + 32 B per leaf
     achieved_gbs = k1_bytes / (k1_avg_ms * 1e-3) / 1e9 if k1_avg_ms > 0 else 0.0
     blocks = blocks_for(local_len, chunk)
-    from deoss_amd.isa import kernel_counts
+    from deoss_amd.isa import chain_instructions_per_block, kernel_counts
     n_local = (local_len + chunk - 1) // chunk
     kind = ctx.leaf_kernel_for(n_local)
     vpb, spb = kernel_counts(kind)
@@ -306,6 +306,14 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
             "clock_ghz": MAX_CLOCK_HZ / 1e9, "blocks_per_leaf": blocks_per_leaf, "floor_ms": round(floor_ms, 3),
             "frac": round(floor_ms / k1_avg_ms, 4),
             "note": "time of one leaf chain at one issue per 4 cycles: the latency-bound kernel's roofline"}
+        ipb = chain_instructions_per_block(kind)
+        if ipb:
+            # the same floor counting every instruction the chain's wave issues (its LDS reads of
+            # -(K+W), loop SALU): one instruction per 4 cycles, whatever its type
+            all_ms = blocks_per_leaf * ipb * ISSUE_CYCLES_ONE_WAVE / MAX_CLOCK_HZ * 1e3
+            out["roofline"]["chain_issue_floor"].update({
+                "instructions_per_block_on_chain": round(ipb, 2), "floor_all_instructions_ms": round(all_ms, 3),
+                "frac_all_instructions": round(all_ms / k1_avg_ms, 4)})
 
     if args.same_device:
         out["ranks"] = world

@@ -169,5 +169,19 @@ def valu_per_block():
     return kernel_counts("wide")
 
 
+def chain_instructions_per_block(kind: str):
+    """All instructions (VALU + LDS + SALU + ...) per block on the leaf's critical wave, from the
+    same ISA counts: a wave issues at most one instruction per turn, whatever its type."""
+    try:
+        with open(COUNTS) as f:
+            d = json.load(f)[kind]
+    except (OSError, KeyError, ValueError):
+        return None
+    w = d if kind == "wide" else d.get("consumer", {})
+    if "total" not in w or not w.get("blocks_per_iteration"):
+        return None
+    return w["total"] / w["blocks_per_iteration"]
+
+
 if __name__ == "__main__":
     print(json.dumps(generate(), indent=1))
