@@ -230,6 +230,7 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
     root_hex = bytes(root_dev.cpu().numpy()).hex() if rank == 0 else None
 
     value = total * args.steps / elapsed / (1 << 30)
+    read_peak_gbs, read_peak_ms = measure_read_peak(ctx, torch, buf, local_len, sptr, stream)
     if world > 1:   # the whole-object buffer is released before the parity legs allocate theirs
         del buf
         torch.cuda.empty_cache()
@@ -295,6 +296,12 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         },
         "root": root_hex,
     }
+    if read_peak_gbs:
+        out["roofline"]["measured_read_peak"] = {
+            "GBps": round(read_peak_gbs, 1), "frac_of_spec": round(read_peak_gbs / HBM_PEAK_GBS, 4),
+            "achieved_frac_of_measured": round(achieved_gbs / read_peak_gbs, 6), "ms": round(read_peak_ms, 4),
+            "bytes": local_len // 16 * 16,
+            "kernel": "read_probe_kernel (dm_read_probe_async: XOR of every word of the same object, one pass)"}
     if kind != "wide" and vpb and k1_avg_ms:
         # The bound that applies to few long leaves: one leaf's serial chain on its consumer wave,
         # which issues at most one VALU instruction every 4 cycles (MI355X_MICROARCH.md, "vector-
@@ -397,6 +404,24 @@ def _summary(r):
     if "cpu_baseline" in r:
         keep["cpu_baseline"] = r["cpu_baseline"]
     return keep
+
+
+def measure_read_peak(ctx, torch, buf, nbytes, sptr, stream, reps=5):
+    """Measured HBM read peak (SURVEY.md 8d asks for it next to the spec): the library's streaming
+    read probe over the timed object itself, HIP events on the launch stream."""
+    n = nbytes // 16 * 16
+    if n < (64 << 20):
+        return None, None
+    x = torch.zeros(1, dtype=torch.int64, device=buf.device)
+    ctx.read_probe_async(buf.data_ptr(), n, x.data_ptr(), sptr)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        ctx.read_probe_async(buf.data_ptr(), n, x.data_ptr(), sptr)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return n / (ms * 1e-3) / 1e9, ms
 
 
 def driver_extras(args, torch, dist, device, dev_index):

@@ -1005,6 +1005,26 @@ int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbyte
     return DM_OK;
 }
 
+int dm_read_probe_async(dm_ctx* ctx, const void* dev, uint64_t nbytes, void* dev_xor8, void* stream) {
+    if (!ctx || !dev_xor8 || (!dev && nbytes) || nbytes % 16 || !is_aligned16(dev) ||
+        reinterpret_cast<uintptr_t>(dev_xor8) % 8)
+        return bad_arg();
+    CallLock lk(ctx->mu);
+    dm_ctx* c = ctx;
+    Dev& d = c->devs[0];
+    hipStream_t s = pick_stream(d, stream);
+    RC_TRY(begin_call(c, d, s));
+    HIP_TRY(hipMemsetAsync(dev_xor8, 0, 8, s));
+    if (nbytes == 0) return DM_OK;
+    const uint64_t n16 = nbytes / 16;
+    // 8 workgroups per CU, whole 4-load rounds per lane where the size allows
+    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(8ull * d.cus, ceil_div(n16, 4 * dm::kBlock)));
+    hipLaunchKernelGGL(dm::read_probe_kernel, dim3((uint32_t)grid), dim3(dm::kBlock), 0, s,
+                       static_cast<const uint8_t*>(dev), n16, static_cast<uint64_t*>(dev_xor8));
+    HIP_TRY(hipGetLastError());
+    return DM_OK;
+}
+
 int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!host && len)) return bad_arg();
     CallLock lk(ctx->mu);

@@ -991,4 +991,34 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint64_t* dst, ui
     }
 }
 
+// HBM read-bandwidth probe (the measured read peak bench.py reports next to the 8 TB/s spec,
+// SURVEY.md 8d): XOR of every 8-byte word of [p, p + 16 * n16), four independent 16-byte loads in
+// flight per lane, grid-stride so consecutive lanes read consecutive 16 B.  One global atomic XOR
+// per workgroup; *out must be zero before the launch.
+__global__ __launch_bounds__(kBlock) void read_probe_kernel(const uint8_t* p, uint64_t n16, uint64_t* out) {
+    const global_u32x4* g = (const global_u32x4*)(p);
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    u32x4_t a = {0u, 0u, 0u, 0u}, b = a, c = a, d = a;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const u32x4_t x0 = g[i], x1 = g[i + stride], x2 = g[i + 2 * stride], x3 = g[i + 3 * stride];
+        a ^= x0;
+        b ^= x1;
+        c ^= x2;
+        d ^= x3;
+    }
+    for (; i < n16; i += stride) a ^= g[i];
+    a ^= b ^ c ^ d;
+    uint64_t v = (((uint64_t)a.y << 32) | a.x) ^ (((uint64_t)a.w << 32) | a.z);
+    for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
+    __shared__ uint64_t part[kBlock / 64];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < kBlock / 64; w++) t ^= part[w];
+        atomicXor(reinterpret_cast<unsigned long long*>(out), (unsigned long long)t);
+    }
+}
+
 }  // namespace dm

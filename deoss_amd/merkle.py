@@ -160,6 +160,11 @@ class MerkleContext:
         self._check(self._L.dm_fill_synthetic_async(self._h, ctypes.c_void_p(dev_ptr), off, nbytes, seed,
                                                     ctypes.c_void_p(stream or None)), "dm_fill_synthetic_async")
 
+    def read_probe_async(self, dev_ptr: int, nbytes: int, dev_xor8: int, stream: int = 0) -> None:
+        """HBM read-bandwidth probe: XOR of every 8-byte word of dev[0, nbytes) into dev_xor8."""
+        self._check(self._L.dm_read_probe_async(self._h, ctypes.c_void_p(dev_ptr), nbytes, ctypes.c_void_p(dev_xor8),
+                                                ctypes.c_void_p(stream or None)), "dm_read_probe_async")
+
     # -- tree levels and proofs (merkletree GetMerklePath / VerifyContent / VerifyTree) ----------
     def tree_node_count(self, n: int) -> int:
         return self._L.dm_tree_node_count(n)

@@ -133,6 +133,12 @@ int dm_root_batch_device_async(dm_ctx *ctx, const void *const *dev_objs, const u
 int dm_fill_synthetic_async(dm_ctx *ctx, void *dev, uint64_t off, uint64_t nbytes, uint64_t seed,
                             void *stream);
 
+/* HBM read-bandwidth probe (measurement utility, not on the reference path): XOR of every 8-byte
+ * little-endian word of dev[0, nbytes) into *dev_xor8 (device memory, zeroed by the call), one
+ * streaming pass.  bench.py times it to report the measured read peak beside the 8 TB/s spec
+ * (SURVEY.md 8d).  dev 16-byte aligned, nbytes a multiple of 16. */
+int dm_read_probe_async(dm_ctx *ctx, const void *dev, uint64_t nbytes, void *dev_xor8, void *stream);
+
 /* ---- Reed-Solomon fragment coding ------------------------------------------
  * The stage after hashing on DeOSS's upload path: cess-go-sdk codes every 32 MiB segment into
  * chain.DataShards = 4 data + chain.ParShards = 8 parity fragments (node/tracker.go:250,369,

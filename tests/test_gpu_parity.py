@@ -327,6 +327,32 @@ def test_leaf_length_above_512MiB(ctx, big_leaves, leaf_mode):
         assert r[32 * k:32 * k + 32] == hashlib.sha256(h + h).digest(), k
 
 
+def test_read_probe_xor(ctx):
+    """The bench's HBM read probe reads every byte exactly once: its XOR of 8-byte words equals
+    numpy's, at sizes around its 4-load rounds and grid-stride tails."""
+    import numpy as np
+    from deoss_amd import DeossMerkleError
+    torch = _torch()
+    s = torch.cuda.current_stream().cuda_stream
+    x = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    for nbytes in (0, 16, 48, 16 * 1023, 16 * 4096 * 4 + 32, (3 << 20) + 16 * 5, 97 << 20):
+        host = np.frombuffer(splitmix64_bytes(nbytes, nbytes + 1), dtype=np.uint64) if nbytes < (4 << 20) else None
+        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+        if host is None:
+            ctx.fill_synthetic_async(buf.data_ptr(), 0, nbytes, nbytes + 1, s)
+            host = buf[:nbytes].cpu().numpy().view(np.uint64)
+        elif nbytes:
+            buf[:nbytes] = torch.from_numpy(host.view(np.uint8).copy()).cuda()
+        ctx.read_probe_async(buf.data_ptr(), nbytes, x.data_ptr(), s)
+        torch.cuda.synchronize()
+        want = int(np.bitwise_xor.reduce(host)) if nbytes else 0
+        assert int(x.cpu().numpy().view(np.uint64)[0]) == want, nbytes
+    with pytest.raises(DeossMerkleError):
+        ctx.read_probe_async(buf.data_ptr(), 24, x.data_ptr(), s)       # not a multiple of 16
+    with pytest.raises(DeossMerkleError):
+        ctx.read_probe_async(buf.data_ptr() + 8, 32, x.data_ptr(), s)   # misaligned
+
+
 def test_empty_and_invalid(ctx):
     from deoss_amd import DeossMerkleError
     with pytest.raises(DeossMerkleError, match="Empty data"):
