@@ -1017,8 +1017,9 @@ int dm_read_probe_async(dm_ctx* ctx, const void* dev, uint64_t nbytes, void* dev
     HIP_TRY(hipMemsetAsync(dev_xor8, 0, 8, s));
     if (nbytes == 0) return DM_OK;
     const uint64_t n16 = nbytes / 16;
-    // 8 workgroups per CU, whole 4-load rounds per lane where the size allows
-    const uint64_t grid = std::max<uint64_t>(1, std::min<uint64_t>(8ull * d.cus, ceil_div(n16, 4 * dm::kBlock)));
+    // 8 workgroups per CU (the measured best, tools/read_peak_ab.hip), at least one load round each
+    const uint64_t grid =
+        std::max<uint64_t>(1, std::min<uint64_t>(8ull * d.cus, ceil_div(n16, dm::kProbeLoads * dm::kBlock)));
     hipLaunchKernelGGL(dm::read_probe_kernel, dim3((uint32_t)grid), dim3(dm::kBlock), 0, s,
                        static_cast<const uint8_t*>(dev), n16, static_cast<uint64_t*>(dev_xor8));
     HIP_TRY(hipGetLastError());

@@ -992,24 +992,31 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint64_t* dst, ui
 }
 
 // HBM read-bandwidth probe (the measured read peak bench.py reports next to the 8 TB/s spec,
-// SURVEY.md 8d): XOR of every 8-byte word of [p, p + 16 * n16), four independent 16-byte loads in
-// flight per lane, grid-stride so consecutive lanes read consecutive 16 B.  One global atomic XOR
-// per workgroup; *out must be zero before the launch.
+// SURVEY.md 8d): XOR of every 8-byte word of [p, p + 16 * n16).  Each workgroup streams one
+// contiguous slab with 16 nontemporal 16-byte loads in flight per lane.  Measured A/B over 8 GiB
+// (tools/read_peak_ab.hip, profiles/r02/r02o_read_ab2.log): grid-stride with 4 loads 5.3 TB/s,
+// slabs 5.7, slabs with nontemporal loads 6.7 TB/s.  One global atomic XOR per workgroup; *out
+// must be zero before the launch.
+constexpr int kProbeLoads = 16;
 __global__ __launch_bounds__(kBlock) void read_probe_kernel(const uint8_t* p, uint64_t n16, uint64_t* out) {
-    const global_u32x4* g = (const global_u32x4*)(p);
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    u32x4_t a = {0u, 0u, 0u, 0u}, b = a, c = a, d = a;
-    for (; i + 3 * stride < n16; i += 4 * stride) {
-        const u32x4_t x0 = g[i], x1 = g[i + stride], x2 = g[i + 2 * stride], x3 = g[i + 3 * stride];
-        a ^= x0;
-        b ^= x1;
-        c ^= x2;
-        d ^= x3;
+    const u32x4_t* g = reinterpret_cast<const u32x4_t*>(p);
+    const uint64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < n16 ? lo + per : n16;
+    u32x4_t acc[kProbeLoads];
+#pragma unroll
+    for (int u = 0; u < kProbeLoads; u++) acc[u] = u32x4_t{0u, 0u, 0u, 0u};
+    uint64_t i = lo + threadIdx.x;
+    for (; i + (kProbeLoads - 1) * kBlock < hi; i += kProbeLoads * kBlock) {
+        u32x4_t x[kProbeLoads];
+#pragma unroll
+        for (int u = 0; u < kProbeLoads; u++) x[u] = __builtin_nontemporal_load(g + i + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < kProbeLoads; u++) acc[u] ^= x[u];
     }
-    for (; i < n16; i += stride) a ^= g[i];
-    a ^= b ^ c ^ d;
-    uint64_t v = (((uint64_t)a.y << 32) | a.x) ^ (((uint64_t)a.w << 32) | a.z);
+    for (; i < hi; i += kBlock) acc[0] ^= g[i];
+#pragma unroll
+    for (int u = 1; u < kProbeLoads; u++) acc[0] ^= acc[u];
+    uint64_t v = (((uint64_t)acc[0].y << 32) | acc[0].x) ^ (((uint64_t)acc[0].w << 32) | acc[0].z);
     for (int m = 32; m >= 1; m >>= 1) v ^= __shfl_xor(v, m, 64);
     __shared__ uint64_t part[kBlock / 64];
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
