@@ -403,7 +403,7 @@ int batch_roots_from_leaves(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* lea
 
 // Leaf hashing of a batch of objects at device addresses + per-object roots.
 int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, const uint64_t* lens, uint64_t nobj,
-                 uint64_t chunk, uint8_t* roots) {
+                 uint64_t chunk, uint8_t* roots, int kind = -1) {
     std::vector<uint64_t> first(nobj + 1, 0);
     for (uint64_t o = 0; o < nobj; o++) {
         if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
@@ -433,11 +433,82 @@ int batch_device(dm_ctx* c, Dev& d, hipStream_t s, const void* const* objs, cons
     la.digests = d.leaves.u8();
     hipEvent_t* tr = timing_record(c, d);
     if (tr) HIP_TRY(hipEventRecord(tr[0], s));
-    RC_TRY(launch_leaves(c, d, s, la, true, aligned, pick_leaf_kernel(c, d, T)));
+    RC_TRY(launch_leaves(c, d, s, la, true, aligned, kind >= 0 ? kind : pick_leaf_kernel(c, d, T)));
     if (tr) HIP_TRY(hipEventRecord(tr[1], s));
     RC_TRY(batch_roots_from_leaves(c, d, s, d.leaves.u8(), first, roots));
     if (tr) HIP_TRY(hipEventRecord(tr[2], s));
     return DM_OK;
+}
+
+// Device-visible addresses of host chunks that all lie in page-locked memory (hipHostMalloc,
+// hipHostRegister): one runtime query per pinned allocation, not per chunk (12,500 queries cost
+// ~30 ms per call).  False if any non-empty chunk is pageable or runs past its allocation.  Empty
+// chunks get the first non-empty chunk's address (the kernels never dereference them).
+bool pinned_view(const void* const* ptrs, const uint64_t* lens, uint64_t n, std::vector<uint64_t>* dev_addr) {
+    uintptr_t lo = 0, hi = 0;
+    uint64_t delta = 0;   // device address = host address + delta inside [lo, hi)
+    bool ok = true;
+    if (dev_addr) dev_addr->assign(n, 0);
+    uint64_t any = 0;
+    for (uint64_t i = 0; i < n && ok; i++) {
+        if (lens[i] == 0) continue;
+        const uintptr_t p = reinterpret_cast<uintptr_t>(ptrs[i]);
+        if (!(p >= lo && p + lens[i] <= hi)) {
+            hipPointerAttribute_t attr{};
+            void* start = nullptr;
+            void* dp = nullptr;
+            ok = hipPointerGetAttributes(&attr, ptrs[i]) == hipSuccess && attr.type == hipMemoryTypeHost &&
+                 hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)ptrs[i]) == hipSuccess &&
+                 start != nullptr && (!dev_addr || (hipHostGetDevicePointer(&dp, start, 0) == hipSuccess && dp));
+            if (!ok) break;
+            // Extent of the allocation.  HIP_POINTER_ATTRIBUTE_RANGE_SIZE comes back truncated to
+            // 32 bits for pinned allocations of 4 GiB and more (0 for torch's 16 GiB block,
+            // measured), so take the larger of it and hipMemPtrGetInfo.  If neither covers the chunk,
+            // accept it when its last byte lies in the same allocation (same range start).
+            const uintptr_t s0 = reinterpret_cast<uintptr_t>(start);
+            size_t size = 0, size2 = 0;
+            if (hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)ptrs[i]) != hipSuccess) size = 0;
+            if (hipMemPtrGetInfo(start, &size2) == hipSuccess && size2 > size) size = size2;
+            uintptr_t end = s0 + size;
+            if (p + lens[i] > end) {
+                void* s_last = nullptr;
+                const void* last = reinterpret_cast<const void*>(p + lens[i] - 1);
+                ok = hipPointerGetAttribute(&s_last, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)last) == hipSuccess &&
+                     s_last == start;
+                end = p + lens[i];
+            }
+            if (!ok) break;
+            lo = s0;
+            hi = end;
+            delta = dev_addr ? reinterpret_cast<uintptr_t>(dp) - s0 : 0;
+        }
+        if (dev_addr) {
+            (*dev_addr)[i] = p + delta;
+            if (!any) any = p + delta;
+        }
+    }
+    (void)hipGetLastError();   // clear the error of an unregistered pointer
+    if (ok && dev_addr)
+        for (uint64_t i = 0; i < n; i++)
+            if (lens[i] == 0) (*dev_addr)[i] = any;
+    return ok;
+}
+
+// Zero-copy: leaves in pinned host memory are read in place by K1Q over PCIe, without a copy
+// to HBM.  K1Q's producer lanes load 8 consecutive 64-byte blocks per leaf, so its reads cross
+// PCIe as whole lines.  Measured from torch-pinned memory (tools/zero_copy_diag.py,
+// profiles/r02/r02s_zc_*.log), zero-copy vs copy: 8 GiB as 256 x 32 MiB 15.81 vs 15.63 GiB/s (the
+// chain rate either way, without the 8 GiB device copy), 8,192 x 1 MiB 53.2 vs 52.4 (PCIe),
+// batches of 1 MiB objects 51.5 vs 43.8 (4,096), 53.2 vs 46.9 (8,192), 49.4 vs 47.6 (12,500).
+// K1L, K1P and K1 reach only ~41 GB/s reading host memory (tools/zero_copy_probe.py), so the
+// many-leaf (wide) regime still copies.  Auto mode only (a forced kernel keeps the copy
+// paths testable); DEOSS_ZERO_COPY=0 turns it off.
+bool zero_copy_regime(const dm_ctx* c, const Dev& d, uint64_t nleaves) {
+    static const bool off = [] {
+        const char* e = std::getenv("DEOSS_ZERO_COPY");
+        return e != nullptr && e[0] == '0';
+    }();
+    return !off && c->leaf_mode == DM_LEAF_AUTO && nleaves > 0 && pick_leaf_kernel(c, d, nleaves) != DM_LEAF_WIDE;
 }
 
 // Copy host chunks to d.data + off[i] (device offsets chosen by the caller, 256-B aligned,
@@ -448,26 +519,7 @@ int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uin
     // Pinned sources (every chunk in page-locked host memory): async copies straight from the
     // caller's buffers, coalescing runs that are contiguous on both sides with no padding between
     // them (so a copy never reads a host byte outside the caller's chunks).
-    // One runtime query per pinned allocation, not per chunk: chunks inside the range of the last
-    // pinned allocation found need no query (12,500 queries cost ~30 ms per call).
-    bool all_pinned = true;
-    uintptr_t lo = 0, hi = 0;
-    for (uint64_t i = 0; i < n && all_pinned; i++) {
-        if (lens[i] == 0) continue;
-        const uintptr_t p = reinterpret_cast<uintptr_t>(ptrs[i]);
-        if (p >= lo && p + lens[i] <= hi) continue;
-        hipPointerAttribute_t attr{};
-        all_pinned = hipPointerGetAttributes(&attr, ptrs[i]) == hipSuccess && attr.type == hipMemoryTypeHost;
-        void* start = nullptr;
-        size_t size = 0;
-        if (all_pinned &&
-            hipPointerGetAttribute(&start, HIP_POINTER_ATTRIBUTE_RANGE_START_ADDR, (hipDeviceptr_t)ptrs[i]) == hipSuccess &&
-            hipPointerGetAttribute(&size, HIP_POINTER_ATTRIBUTE_RANGE_SIZE, (hipDeviceptr_t)ptrs[i]) == hipSuccess) {
-            lo = reinterpret_cast<uintptr_t>(start);
-            hi = lo + size;
-        }
-    }
-    (void)hipGetLastError();
+    const bool all_pinned = pinned_view(ptrs, lens, n, nullptr);
     if (all_pinned) {
         uint64_t i = 0;
         while (i < n) {
@@ -540,6 +592,14 @@ int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens
 int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint64_t chunk) {
     const uint64_t n = ceil_div(len, chunk);
     const uint64_t last_len = len - (n - 1) * chunk;
+    std::vector<uint64_t> view;
+    if (zero_copy_regime(c, d, n) && pinned_view(&host, &len, 1, &view)) {
+        HIP_TRY(d.leaves.ensure(n * 32));
+        dm::LeafArgs la = uniform_args(reinterpret_cast<const void*>(view[0]), len, chunk);
+        la.byte_end = ~0ull;
+        la.digests = d.leaves.u8();
+        return launch_leaves(c, d, d.stream, la, false, view[0] % 16 == 0 && chunk % 16 == 0, DM_LEAF_QUAD);
+    }
     HIP_TRY(d.data.ensure(len));
     HIP_TRY(d.leaves.ensure(n * 32));
     hipPointerAttribute_t attr{};
@@ -1050,7 +1110,10 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));
     std::vector<uint64_t> addr;
-    RC_TRY(pack_chunks(c, d, ptrs, lens, n, addr));
+    const bool zc = zero_copy_regime(c, d, n) && pinned_view(ptrs, lens, n, &addr);
+    if (!zc) RC_TRY(pack_chunks(c, d, ptrs, lens, n, addr));
+    bool aligned = true;
+    for (uint64_t i = 0; i < n && zc; i++) aligned &= addr[i] % 16 == 0;
     RC_TRY(tables_begin(c, d, n * 16 + 1024));
     HIP_TRY(d.leaves.ensure(n * 32));
     RC_TRY(upload(c, d, d.stream, d.tab_addr, addr.data(), n * 8));
@@ -1061,7 +1124,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
     la.nleaves = n;
     la.byte_end = ~0ull;
     la.digests = d.leaves.u8();
-    RC_TRY(launch_leaves(c, d, d.stream, la, true, true, pick_leaf_kernel(c, d, n)));
+    RC_TRY(launch_leaves(c, d, d.stream, la, true, aligned, zc ? DM_LEAF_QUAD : pick_leaf_kernel(c, d, n)));
     return reduce_leaves_to_host(c, d, n, leaf_out, root);
 }
 
@@ -1077,12 +1140,15 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
     }
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));
+    uint64_t T = 0;
+    for (uint64_t o = 0; o < nobj; o++) T += ceil_div(lens[o], chunk);
     std::vector<uint64_t> addr;
-    RC_TRY(pack_chunks(c, d, objs, lens, nobj, addr));
+    const bool zc = zero_copy_regime(c, d, T) && pinned_view(objs, lens, nobj, &addr);
+    if (!zc) RC_TRY(pack_chunks(c, d, objs, lens, nobj, addr));
     std::vector<const void*> dptr(nobj);
     for (uint64_t o = 0; o < nobj; o++) dptr[o] = reinterpret_cast<const void*>(addr[o]);
     HIP_TRY(d.gather.ensure(nobj * 32));
-    RC_TRY(batch_device(c, d, d.stream, dptr.data(), lens, nobj, chunk, d.gather.u8()));
+    RC_TRY(batch_device(c, d, d.stream, dptr.data(), lens, nobj, chunk, d.gather.u8(), zc ? DM_LEAF_QUAD : -1));
     HIP_TRY(hipMemcpyAsync(roots, d.gather.p, nobj * 32, hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
     return DM_OK;
