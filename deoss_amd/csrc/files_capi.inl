@@ -211,38 +211,54 @@ int files_leaves(dm_ctx* c, Dev& d, const FileSet& fs, uint64_t l0, uint64_t l1)
         la.lens = static_cast<const uint64_t*>(d.tab_len.p);
         return launch_leaves(c, d, s, la, true, true, kind);
     }
-    // striped: file i's bytes [j*W, (j+1)*W) arrive in step j; row i of the HBM image has pitch P
+    // striped: file i's bytes [j*W, (j+1)*W) arrive in step j.  Copy mode: row i of the HBM image
+    // has pitch P.  Zero-copy mode (auto, latency regime: zero_copy_regime): K1Q reads each stripe
+    // straight out of the pinned staging slot it was pread into, no H2D copy and no HBM image
+    // (profiles/r02/r02v_*.log); a slot is refilled once the launch that read it has finished.
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
     const uint64_t nsteps = ceil_div(maxlen, W), P = nsteps * W;
-    HIP_TRY(d.data.ensure(n * P));
+    const bool zc = zero_copy_regime(c, d, n);
     HIP_TRY(d.nodes_b.ensure(n * 32));   // chaining state between stripes (8 words per leaf)
-    std::vector<uint64_t> addr(nsteps * n), lens(n);
-    for (uint64_t i = 0; i < n; i++) lens[i] = fs.size[l0 + i];
-    for (uint64_t j = 0; j < nsteps; j++)   // the kernel expects each leaf's pointer at byte j*W
-        for (uint64_t i = 0; i < n; i++) addr[j * n + i] = reinterpret_cast<uint64_t>(d.data.u8() + i * P + j * W);
-    RC_TRY(tables_begin(c, d, (nsteps + 1) * n * 8 + 1024));
-    RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), nsteps * n * 8));
-    RC_TRY(upload(c, d, s, d.tab_len, lens.data(), n * 8));
     HIP_TRY(d.stage[0].ensure(n * W));
     HIP_TRY(d.stage[1].ensure(n * W));
+    std::vector<uint64_t> addr(zc ? 2 * n : nsteps * n), lens(n);
+    for (uint64_t i = 0; i < n; i++) lens[i] = fs.size[l0 + i];
+    if (zc) {
+        for (int k = 0; k < 2; k++) {
+            void* dp = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&dp, d.stage[k].p, 0));
+            for (uint64_t i = 0; i < n; i++) addr[k * n + i] = reinterpret_cast<uint64_t>(dp) + i * W;
+        }
+    } else {
+        HIP_TRY(d.data.ensure(n * P));
+        for (uint64_t jj = 0; jj < nsteps; jj++)   // the kernel expects each leaf's pointer at byte j*W
+            for (uint64_t i = 0; i < n; i++) addr[jj * n + i] = reinterpret_cast<uint64_t>(d.data.u8() + i * P + jj * W);
+    }
+    RC_TRY(tables_begin(c, d, (addr.size() + n) * 8 + 1024));
+    RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), addr.size() * 8));
+    RC_TRY(upload(c, d, s, d.tab_len, lens.data(), n * 8));
     bool busy[2] = {false, false};
     la.lens = static_cast<const uint64_t*>(d.tab_len.p);
     la.state = static_cast<uint32_t*>(d.nodes_b.p);
-    for (uint64_t j = 0, slot = 0; j < nsteps; j++, slot ^= 1) {
-        if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
+    for (uint64_t jj = 0, slot = 0; jj < nsteps; jj++, slot ^= 1) {
+        hipEvent_t slot_free = zc ? d.ev_step[slot] : d.ev_copy[slot];
+        if (busy[slot]) HIP_TRY(hipEventSynchronize(slot_free));
         uint8_t* st = d.stage[slot].u8();
         std::vector<FilePart> parts;
         for (uint64_t i = 0; i < n; i++)
-            if (lens[i] > j * W) parts.push_back({l0 + i, j * W, std::min(W, lens[i] - j * W), st + i * W});
+            if (lens[i] > jj * W) parts.push_back({l0 + i, jj * W, std::min(W, lens[i] - jj * W), st + i * W});
         RC_TRY(read_parts(c, fs, parts));
-        HIP_TRY(hipMemcpy2DAsync(d.data.u8() + j * W, P, st, W, W, n, hipMemcpyHostToDevice, d.copy));
-        HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
+        if (!zc) {
+            HIP_TRY(hipMemcpy2DAsync(d.data.u8() + jj * W, P, st, W, W, n, hipMemcpyHostToDevice, d.copy));
+            HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
+            HIP_TRY(hipStreamWaitEvent(s, d.ev_copy[slot], 0));
+        }
+        la.addrs = static_cast<const uint64_t*>(d.tab_addr.p) + (zc ? slot : jj) * n;
+        la.byte_off = jj * W;
+        la.byte_end = (jj + 1) * W;
+        RC_TRY(launch_leaves(c, d, s, la, true, true, zc ? DM_LEAF_QUAD : kind));
+        if (zc) HIP_TRY(hipEventRecord(d.ev_step[slot], s));
         busy[slot] = true;
-        HIP_TRY(hipStreamWaitEvent(s, d.ev_copy[slot], 0));
-        la.addrs = static_cast<const uint64_t*>(d.tab_addr.p) + j * n;
-        la.byte_off = j * W;
-        la.byte_end = (j + 1) * W;
-        RC_TRY(launch_leaves(c, d, s, la, true, true, kind));
     }
     return DM_OK;
 }

@@ -130,3 +130,22 @@ def test_zero_copy_allocation_above_4GiB(auto_ctx, oracle_lib):
     want_leaves, want = oracle_lib.root_buffer_ptr(addr, length, chunk, 8, True)
     leaves, root = auto_ctx.root_buffer_ptr(addr, length, chunk, want_leaves=True)
     assert root == want and leaves == want_leaves
+
+
+def test_zero_copy_files_striped(auto_ctx, oracle_lib, tmp_path):
+    """NewHashTree over files larger than one stripe budget in auto mode: every stripe is hashed
+    straight out of the pinned staging slot it was read into (ragged sizes, an empty file)."""
+    sizes = [(17 << 20) + 5, 16 << 20, 0, (16 << 20) - 3, 1] + [(15 << 20) + 4096 * i for i in range(14)]
+    paths, blobs = [], []
+    for i, n in enumerate(sizes):
+        data = oracle_lib.splitmix_bytes(n, 900 + i) if n else b""
+        p = tmp_path / f"seg{i:02d}"
+        p.write_bytes(data)
+        paths.append(str(p))
+        blobs.append(data)
+    assert sum(sizes) > (256 << 20)
+    leaves, root = auto_ctx.new_hash_tree(paths)
+    from oracle import py_root_chunks
+    want_leaves, want = py_root_chunks(blobs)
+    assert root == want
+    assert leaves == want_leaves
