@@ -4,7 +4,7 @@ The compute path is ``libdeoss_merkle.so`` (hand-written HIP for gfx950, C ABI i
 ``include/deoss_merkle.h``); this package is its host-side mirror of the reference Go API.
 """
 from ._lib import DeossMerkleError, LIB_PATH, load_library  # noqa: F401
-from .merkle import MerkleContext  # noqa: F401
+from .merkle import MerkleContext, PinnedBuffer  # noqa: F401
 from .hashtree import (  # noqa: F401
     HashTreeContent, Init, MerkleTree, NewHashTree, NewHashTreeFromBuffer, NewHashTreesBatch, NewStream, Node,
     Stream,

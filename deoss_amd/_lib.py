@@ -29,7 +29,8 @@ EXPORTS = (
     "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count", "dm_gpu_count",
     "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
     "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
-    "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_read_probe_async", "dm_set_leaf_kernel", "dm_leaf_kernel_for",
+    "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_read_probe_async", "dm_host_alloc",
+    "dm_host_free", "dm_set_leaf_kernel", "dm_leaf_kernel_for",
     "dm_set_timing", "dm_stream_open", "dm_stream_write", "dm_stream_close", "dm_stream_abort",
     "dm_stream_error",
     "dm_timing_summary",
@@ -75,6 +76,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_root_batch_device_async": ([vp, pvp, pu64, u64, u64, vp, vp], i32),
         "dm_fill_synthetic_async": ([vp, vp, u64, u64, u64, vp], i32),
         "dm_read_probe_async": ([vp, vp, u64, vp, vp], i32),
+        "dm_host_alloc": ([u64, ctypes.POINTER(vp)], i32),
+        "dm_host_free": ([vp], None),
         "dm_stream_open": ([vp, u64, ctypes.POINTER(vp)], i32),
         "dm_stream_write": ([vp, vp, u64], i32),
         "dm_stream_close": ([vp, vp, u64, pu64, vp], i32),

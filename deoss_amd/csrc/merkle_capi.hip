@@ -893,6 +893,23 @@ int dm_gpu_count(void) {
     return n;
 }
 
+int dm_host_alloc(uint64_t bytes, void** out) {
+    if (!out || bytes == 0) return bad_arg();
+    *out = nullptr;
+    DeviceRestore dev;
+    const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocPortable);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        (void)hipGetLastError();
+        return set_err(e == hipErrorOutOfMemory ? DM_ERR_NOMEM : DM_ERR_HIP, "dm_host_alloc: hipHostMalloc failed");
+    }
+    return DM_OK;
+}
+
+void dm_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
 int dm_create(dm_ctx** out, const int* devs, int ndev) {
     if (!out) return bad_arg();
     *out = nullptr;

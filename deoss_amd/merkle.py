@@ -348,3 +348,27 @@ class MerkleStream:
             self.abort()
         except Exception:
             pass
+
+
+class PinnedBuffer:
+    """Page-locked host memory from dm_host_alloc (visible to every GPU).  Objects held in it are
+    hashed in place by the zero-copy host paths (dm_root_buffer / chunks / batch).  `array()` is a
+    writable numpy view; free() (or garbage collection) releases it."""
+
+    def __init__(self, nbytes: int):
+        self._L = load_library()
+        p = ctypes.c_void_p()
+        rc = self._L.dm_host_alloc(nbytes, ctypes.byref(p))
+        if rc != 0:
+            raise DeossMerkleError(rc, (self._L.dm_last_error(None) or b"").decode() or "dm_host_alloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+        self._fin = weakref.finalize(self, self._L.dm_host_free, ctypes.c_void_p(self.ptr))
+
+    def array(self):
+        import numpy as np
+        return np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+
+    def free(self) -> None:
+        self._fin()
+        self.ptr = None

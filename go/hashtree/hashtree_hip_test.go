@@ -83,3 +83,22 @@ func TestStreamGPU(t *testing.T) {
 	_, err = aborted.Close()
 	assert.Error(t, err)
 }
+
+// A body read into pinned memory hashes in place (zero-copy) to the same tree as a Go slice.
+func TestPinnedBufferZeroCopy(t *testing.T) {
+	b, err := NewPinnedBuffer(8<<20 + 77)
+	assert.NoError(t, err)
+	defer b.Free()
+	body := b.Bytes()
+	for i := range body {
+		body[i] = byte(i*7 + i>>11)
+	}
+	goCopy := append([]byte(nil), body...)
+	want, err := NewHashTreeFromBuffer(goCopy, 1<<20)
+	assert.NoError(t, err)
+	got, err := NewHashTreeFromBuffer(body, 1<<20)
+	assert.NoError(t, err)
+	assert.Equal(t, want.MerkleRoot(), got.MerkleRoot())
+	_, err = NewPinnedBuffer(0)
+	assert.Error(t, err)
+}

@@ -6,8 +6,8 @@
 //   MerkleTree{Leafs, MerkleRoot()}                  cbergoon/merkletree v0.2.0 (go.mod:10)
 // Leafs has n entries, n+1 when n is odd (last leaf duplicated, dup = true), as merkletree's
 // buildWithContent makes it.  Interior nodes are not materialised (the GPU reduces the tree).
-// Also the Go package's additions: Init / DEOSS_GPUS (every GPU by default), NewHashTreeFromBuffer
-// and the hash-while-receiving Stream.  Header-only; link with -ldeoss_merkle.
+// Also the Go package's additions: Init / DEOSS_GPUS (every GPU by default), NewHashTreeFromBuffer,
+// PinnedBuffer (zero-copy host memory) and the hash-while-receiving Stream.  Header-only; link with -ldeoss_merkle.
 #pragma once
 
 #include <array>
@@ -165,6 +165,28 @@ inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTreeF
     if (rc != DM_OK) return {nullptr, make_error(cx.get(), rc)};
     return {build(leaves, root), std::nullopt};
 }
+
+// Page-locked host memory (dm_host_alloc), as the Go PinnedBuffer: an object read into it is hashed
+// in place by NewHashTreeFromBuffer (zero-copy: the leaf kernel reads it over PCIe).
+class PinnedBuffer {
+  public:
+    static std::pair<std::unique_ptr<PinnedBuffer>, std::optional<Error>> New(uint64_t n) {
+        void* p = nullptr;
+        const int rc = dm_host_alloc(n, &p);
+        if (rc != DM_OK) return {nullptr, make_error(nullptr, rc)};
+        return {std::unique_ptr<PinnedBuffer>(new PinnedBuffer(p, n)), std::nullopt};
+    }
+    uint8_t* data() const { return static_cast<uint8_t*>(p_); }
+    uint64_t size() const { return n_; }
+    ~PinnedBuffer() { dm_host_free(p_); }
+    PinnedBuffer(const PinnedBuffer&) = delete;
+    PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+
+  private:
+    PinnedBuffer(void* p, uint64_t n) : p_(p), n_(n) {}
+    void* p_;
+    uint64_t n_;
+};
 
 // Hash-while-receiving, as the Go Stream (go/hashtree/stream_hip.go): Write pieces of any size,
 // Close() returns the tree NewHashTreeFromBuffer builds over the concatenated bytes, Abort()

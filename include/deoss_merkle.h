@@ -63,6 +63,15 @@ int dm_device_count(dm_ctx *ctx);
  * default to every GPU of the node: dm_create(ctx, {0 .. dm_gpu_count()-1}, n). */
 int dm_gpu_count(void);
 
+/* Page-locked host memory, visible to every GPU, for callers that want the zero-copy host paths.
+ * dm_root_buffer / dm_root_chunks / dm_root_batch hash an object held in such memory in place: K1Q
+ * reads it over PCIe, with no H2D copy and no HBM copy, whenever the leaf count is in the latency
+ * regime.  A Go upload handler, for example, reads the request body into it
+ * (go/hashtree/pinned_hip.go).  Free with dm_host_free.  Any hipHostMalloc / hipHostRegister /
+ * torch pin_memory buffer works the same way. */
+int dm_host_alloc(uint64_t bytes, void **out);
+void dm_host_free(void *p);
+
 /* ---- host-memory entry points (synchronous) ---------------------------------------------- */
 
 /* NewHashTree(chunkPath) (types.go:19-39): each file is one leaf, read whole, in order, with Go's

@@ -103,6 +103,17 @@ int main(int argc, char** argv) {
     auto [sb, esb] = hashtree::Stream::New(100);
     EXPECT(!sb && esb && esb->code == DM_ERR_INVALID);
 
+    // PinnedBuffer: the same body hashed in place from page-locked memory (zero-copy path)
+    auto [pb, epb] = hashtree::PinnedBuffer::New(body.size());
+    EXPECT(!epb && pb);
+    if (pb) {
+        std::memcpy(pb->data(), body.data(), body.size());
+        auto [tp, etp] = hashtree::NewHashTreeFromBuffer(pb->data(), pb->size(), 4096);
+        EXPECT(!etp && tp && whole && tp->MerkleRoot() == whole->MerkleRoot());
+    }
+    auto [p0, ep0] = hashtree::PinnedBuffer::New(0);
+    EXPECT(!p0 && ep0 && ep0->code == DM_ERR_INVALID);
+
     if (fails) return 1;
     std::printf("PASS\n");
     return 0;

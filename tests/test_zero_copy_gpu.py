@@ -149,3 +149,18 @@ def test_zero_copy_files_striped(auto_ctx, oracle_lib, tmp_path):
     want_leaves, want = py_root_chunks(blobs)
     assert root == want
     assert leaves == want_leaves
+
+
+def test_pinned_buffer_api(auto_ctx, oracle_lib):
+    """dm_host_alloc / dm_host_free (PinnedBuffer): an object written into it hashes in place."""
+    from deoss_amd import DeossMerkleError, PinnedBuffer
+    n = (24 << 20) + 99
+    pb = PinnedBuffer(n)
+    arr = pb.array()
+    arr[:] = np.frombuffer(oracle_lib.splitmix_bytes(n, 31), dtype=np.uint8)
+    leaves, root = auto_ctx.root_buffer_ptr(pb.ptr, n, 1 << 20, want_leaves=True)
+    want_leaves, want = oracle_lib.root_buffer_ptr(pb.ptr, n, 1 << 20, 4, True)
+    assert root == want and leaves == want_leaves
+    pb.free()
+    with pytest.raises(DeossMerkleError):
+        PinnedBuffer(0)
