@@ -216,23 +216,34 @@ int files_leaves(dm_ctx* c, Dev& d, const FileSet& fs, uint64_t l0, uint64_t l1)
     // straight out of the pinned staging slot it was pread into, no H2D copy and no HBM image
     // (profiles/r02/r02v_*.log); a slot is refilled once the launch that read it has finished.
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
-    const uint64_t nsteps = ceil_div(maxlen, W), P = nsteps * W;
+    // Stripe schedule: the first stripe's reads overlap nothing (the GPU waits for them), so the
+    // stripes start at W/16 and grow by 1/8 per step up to W.  A stripe's reads must finish within
+    // the previous stripe's hashing; reads from the page cache run ~1.2x the chain-bound hash rate
+    // at 256 x 32 MiB.  Offsets and widths are multiples of 64 (whole blocks).
+    std::vector<uint64_t> so, sw;
+    for (uint64_t off = 0, w = std::max<uint64_t>(64, (W / 16) / 64 * 64); off < maxlen;) {
+        so.push_back(off);
+        sw.push_back(w);
+        off += w;
+        w = std::min(W, std::max(w + 64, (w + w / 8) / 64 * 64));
+    }
+    const uint64_t nsteps = so.size(), P = so.back() + sw.back();
     const bool zc = zero_copy_regime(c, d, n);
     HIP_TRY(d.nodes_b.ensure(n * 32));   // chaining state between stripes (8 words per leaf)
     HIP_TRY(d.stage[0].ensure(n * W));
     HIP_TRY(d.stage[1].ensure(n * W));
     std::vector<uint64_t> addr(zc ? 2 * n : nsteps * n), lens(n);
     for (uint64_t i = 0; i < n; i++) lens[i] = fs.size[l0 + i];
-    if (zc) {
+    if (zc) {   // staging slot k: row i (W bytes) holds leaf i's current stripe
         for (int k = 0; k < 2; k++) {
             void* dp = nullptr;
             HIP_TRY(hipHostGetDevicePointer(&dp, d.stage[k].p, 0));
             for (uint64_t i = 0; i < n; i++) addr[k * n + i] = reinterpret_cast<uint64_t>(dp) + i * W;
         }
-    } else {
+    } else {    // HBM image, row pitch P; the kernel expects each leaf's pointer at its stripe's offset
         HIP_TRY(d.data.ensure(n * P));
-        for (uint64_t jj = 0; jj < nsteps; jj++)   // the kernel expects each leaf's pointer at byte j*W
-            for (uint64_t i = 0; i < n; i++) addr[jj * n + i] = reinterpret_cast<uint64_t>(d.data.u8() + i * P + jj * W);
+        for (uint64_t jj = 0; jj < nsteps; jj++)
+            for (uint64_t i = 0; i < n; i++) addr[jj * n + i] = reinterpret_cast<uint64_t>(d.data.u8() + i * P + so[jj]);
     }
     RC_TRY(tables_begin(c, d, (addr.size() + n) * 8 + 1024));
     RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), addr.size() * 8));
@@ -246,16 +257,16 @@ int files_leaves(dm_ctx* c, Dev& d, const FileSet& fs, uint64_t l0, uint64_t l1)
         uint8_t* st = d.stage[slot].u8();
         std::vector<FilePart> parts;
         for (uint64_t i = 0; i < n; i++)
-            if (lens[i] > jj * W) parts.push_back({l0 + i, jj * W, std::min(W, lens[i] - jj * W), st + i * W});
+            if (lens[i] > so[jj]) parts.push_back({l0 + i, so[jj], std::min(sw[jj], lens[i] - so[jj]), st + i * W});
         RC_TRY(read_parts(c, fs, parts));
         if (!zc) {
-            HIP_TRY(hipMemcpy2DAsync(d.data.u8() + jj * W, P, st, W, W, n, hipMemcpyHostToDevice, d.copy));
+            HIP_TRY(hipMemcpy2DAsync(d.data.u8() + so[jj], P, st, W, sw[jj], n, hipMemcpyHostToDevice, d.copy));
             HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
             HIP_TRY(hipStreamWaitEvent(s, d.ev_copy[slot], 0));
         }
         la.addrs = static_cast<const uint64_t*>(d.tab_addr.p) + (zc ? slot : jj) * n;
-        la.byte_off = jj * W;
-        la.byte_end = (jj + 1) * W;
+        la.byte_off = so[jj];
+        la.byte_end = so[jj] + sw[jj];
         RC_TRY(launch_leaves(c, d, s, la, true, true, zc ? DM_LEAF_QUAD : kind));
         if (zc) HIP_TRY(hipEventRecord(d.ev_step[slot], s));
         busy[slot] = true;
