@@ -216,17 +216,8 @@ int files_leaves(dm_ctx* c, Dev& d, const FileSet& fs, uint64_t l0, uint64_t l1)
     // straight out of the pinned staging slot it was pread into, no H2D copy and no HBM image
     // (profiles/r02/r02v_*.log); a slot is refilled once the launch that read it has finished.
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
-    // Stripe schedule: the first stripe's reads overlap nothing (the GPU waits for them), so the
-    // stripes start at W/16 and grow by 1/8 per step up to W.  A stripe's reads must finish within
-    // the previous stripe's hashing; reads from the page cache run ~1.2x the chain-bound hash rate
-    // at 256 x 32 MiB.  Offsets and widths are multiples of 64 (whole blocks).
-    std::vector<uint64_t> so, sw;
-    for (uint64_t off = 0, w = std::max<uint64_t>(64, (W / 16) / 64 * 64); off < maxlen;) {
-        so.push_back(off);
-        sw.push_back(w);
-        off += w;
-        w = std::min(W, std::max(w + 64, (w + w / 8) / 64 * 64));
-    }
+    std::vector<uint64_t> so, sw;   // ramped stripes (stripe_schedule)
+    stripe_schedule(W, maxlen, so, sw);
     const uint64_t nsteps = so.size(), P = so.back() + sw.back();
     const bool zc = zero_copy_regime(c, d, n);
     HIP_TRY(d.nodes_b.ensure(n * 32));   // chaining state between stripes (8 words per leaf)
