@@ -62,6 +62,40 @@ def default_context() -> MerkleContext:
     return _default_ctx
 
 
+# NewHashTreeFromBuffer objects up to BATCH_LIMIT bytes go through a process-wide coalescing
+# dm_batcher per chunk size, as the Go package does (go/hashtree/types_hip.go): concurrent callers
+# share GPU passes instead of queueing one chain-latency pass each.  Larger
+# objects take dm_root_buffer on the default context (ramped striped H2D, zero-copy when pinned,
+# sharded over its GPUs).
+BATCH_LIMIT = 256 << 20
+_batchers: dict = {}
+_batch_lock = None
+
+
+def _batcher(chunk: int):
+    global _batch_lock
+    import threading
+    if _batch_lock is None:
+        _batch_lock = threading.Lock()
+    with _batch_lock:
+        b = _batchers.get(chunk)
+        if b is None:
+            import atexit
+            from .batcher import ROOT, Batcher
+            default_context()   # fixes the device list (Init after this point is refused)
+            b = Batcher(ROOT, chunk, device=_device_list(), linger_us=2000)
+            _batchers[chunk] = b
+            if len(_batchers) == 1:
+                atexit.register(_close_batchers)
+        return b
+
+
+def _close_batchers() -> None:
+    for b in list(_batchers.values()):
+        b.close()
+    _batchers.clear()
+
+
 class HashTreeContent:
     """Leaf payload (hashtree.go:18-20).  ``x`` holds the chunk bytes (or None if dropped)."""
 
@@ -211,7 +245,10 @@ def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContex
         return None, DeossMerkleError(-1, "Empty data")
     c = ctx or default_context()
     try:
-        leaves, root = c.root_buffer(buf, chunkSize, want_leaves=True)
+        if ctx is None and len(buf) <= BATCH_LIMIT:
+            leaves, root = _batcher(chunkSize).root(buf, want_leaves=True)
+        else:
+            leaves, root = c.root_buffer(buf, chunkSize, want_leaves=True)
     except DeossMerkleError as e:
         return None, e
     n = len(leaves) // 32

@@ -7,6 +7,7 @@ import (
 	"encoding/hex"
 	"os"
 	"path/filepath"
+	"sync"
 	"testing"
 
 	"github.com/stretchr/testify/assert"
@@ -101,4 +102,30 @@ func TestPinnedBufferZeroCopy(t *testing.T) {
 	assert.Equal(t, want.MerkleRoot(), got.MerkleRoot())
 	_, err = NewPinnedBuffer(0)
 	assert.Error(t, err)
+}
+
+// Concurrent handler goroutines (the batcher path) get the trees a single call gives.
+func TestFromBufferConcurrent(t *testing.T) {
+	var wg sync.WaitGroup
+	for g := 0; g < 32; g++ {
+		wg.Add(1)
+		go func(g int) {
+			defer wg.Done()
+			body := make([]byte, 3<<20+g*4099)
+			for i := range body {
+				body[i] = byte(i*13 + g)
+			}
+			got, err := NewHashTreeFromBuffer(body, 1<<20)
+			assert.NoError(t, err)
+			var leaves [][32]byte
+			for o := 0; o < len(body); o += 1 << 20 {
+				leaves = append(leaves, sha256.Sum256(body[o:min(o+1<<20, len(body))]))
+			}
+			assert.Equal(t, len(leaves)+len(leaves)%2, len(got.Leafs))
+			for i := range leaves {
+				assert.Equal(t, leaves[i][:], got.Leafs[i].Hash)
+			}
+		}(g)
+	}
+	wg.Wait()
 }

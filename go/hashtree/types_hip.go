@@ -162,6 +162,47 @@ func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error) {
 	return buildTree(leaves, root)
 }
 
+// BatchLimit: NewHashTreeFromBuffer objects up to this size go through a process-wide coalescing
+// dm_batcher per chunk size, so concurrent handler goroutines share GPU passes instead of
+// queueing one chain-latency pass each on the context (DESIGN.md §6.9: 131x for 256 concurrent
+// 1 MiB uploads).  Larger objects take dm_root_buffer: ramped striped H2D overlapped with
+// hashing, zero-copy from pinned memory, sharded over the context's GPUs.
+const BatchLimit = 256 << 20
+
+var (
+	batchMu  sync.Mutex
+	batchers = map[int]*C.dm_batcher{}
+)
+
+func batcherFor(chunk int) (*C.dm_batcher, error) {
+	if _, err := gpu(); err != nil { // fixes the device list
+		return nil, err
+	}
+	batchMu.Lock()
+	defer batchMu.Unlock()
+	if b, ok := batchers[chunk]; ok {
+		return b, nil
+	}
+	devs, err := deviceList()
+	if err != nil {
+		return nil, err
+	}
+	cdevs := make([]C.int, len(devs))
+	for i, d := range devs {
+		cdevs[i] = C.int(d)
+	}
+	runtime.LockOSThread() // dm_batcher_last_error is thread-local
+	defer runtime.UnlockOSThread()
+	var b *C.dm_batcher
+	// 2 worker slots per GPU, 4,096 leaves per batch, 2 ms linger
+	if rc := C.dm_batcher_create(&cdevs[0], C.int(len(cdevs)), C.DM_BATCH_ROOT, C.uint64_t(chunk), 0, 0, 0, 0, 0, 2000,
+		&b); rc != C.DM_OK {
+		return nil, errors.New(C.GoString(C.dm_batcher_last_error()))
+	}
+	batchers[chunk] = b
+	return b, nil
+}
+
 // NewHashTreeFromBuffer (additive): the upload body already in memory, split into chunkSize
 // chunks (the last one short) -- no temp files, one H2D pass.
 func NewHashTreeFromBuffer(buf []byte, chunkSize int) (*merkletree.MerkleTree, error) {
@@ -171,13 +212,30 @@ func NewHashTreeFromBuffer(buf []byte, chunkSize int) (*merkletree.MerkleTree, e
 	if len(buf) == 0 {
 		return nil, errors.New("Empty data")
 	}
+	n := (len(buf) + chunkSize - 1) / chunkSize
+	leaves := make([]byte, 32*n)
+	root := make([]byte, 32)
+	if len(buf) <= BatchLimit {
+		b, err := batcherFor(chunkSize)
+		if err != nil {
+			return nil, err
+		}
+		runtime.LockOSThread()
+		defer runtime.UnlockOSThread()
+		rc := C.dm_batcher_root(b, unsafe.Pointer(&buf[0]), C.uint64_t(len(buf)),
+			(*C.uint8_t)(unsafe.Pointer(&leaves[0])), (*C.uint8_t)(unsafe.Pointer(&root[0])))
+		if rc != C.DM_OK {
+			if rc == C.DM_ERR_EMPTY {
+				return nil, errors.New("Empty data")
+			}
+			return nil, errors.New(C.GoString(C.dm_batcher_last_error()))
+		}
+		return buildTree(leaves, root)
+	}
 	c, err := gpu()
 	if err != nil {
 		return nil, err
 	}
-	n := (len(buf) + chunkSize - 1) / chunkSize
-	leaves := make([]byte, 32*n)
-	root := make([]byte, 32)
 	runtime.LockOSThread()
 	defer runtime.UnlockOSThread()
 	rc := C.dm_root_buffer(c, unsafe.Pointer(&buf[0]), C.uint64_t(len(buf)), C.uint64_t(chunkSize),

@@ -13,7 +13,9 @@
 #include <array>
 #include <cstdint>
 #include <cstdlib>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <optional>
 #include <string>
 #include <utility>
@@ -151,6 +153,40 @@ inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTree(
     return {build(leaves, root), std::nullopt};
 }
 
+// Objects up to kBatchLimit bytes go through a process-wide coalescing dm_batcher per chunk size,
+// as the Go package does: concurrent callers share GPU passes.  Larger ones take
+// dm_root_buffer on the context (ramped striped H2D, zero-copy when pinned, sharded over its GPUs).
+constexpr uint64_t kBatchLimit = 256ull << 20;
+
+class Batchers {
+  public:
+    static Batchers& instance() {
+        static Batchers b;
+        return b;
+    }
+    // The batcher for `chunk` (created on first use over the context's GPUs), or an error.
+    std::pair<dm_batcher*, std::optional<Error>> get(uint64_t chunk) {
+        std::lock_guard<std::mutex> lk(mu_);
+        auto it = m_.find(chunk);
+        if (it != m_.end()) return {it->second, std::nullopt};
+        const std::vector<int> devs = device_list();
+        dm_batcher* b = nullptr;
+        // 2 worker slots per GPU, 4,096 leaves per batch, 2 ms linger
+        const int rc = dm_batcher_create(devs.data(), (int)devs.size(), DM_BATCH_ROOT, chunk, 0, 0, 0, 0, 0, 2000, &b);
+        if (rc != DM_OK) return {nullptr, Error{rc, dm_batcher_last_error()}};
+        m_[chunk] = b;
+        return {b, std::nullopt};
+    }
+    ~Batchers() {
+        for (auto& kv : m_) dm_batcher_destroy(kv.second);
+    }
+
+  private:
+    Batchers() { (void)Context::instance(); }   // fixes the device list; destroyed before it
+    std::mutex mu_;
+    std::map<uint64_t, dm_batcher*> m_;
+};
+
 // Additive: one in-memory object split into chunkSize chunks (the upload-handler buffer).
 inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTreeFromBuffer(
     const void* buf, uint64_t len, int64_t chunkSize) {
@@ -161,6 +197,14 @@ inline std::pair<std::unique_ptr<MerkleTree>, std::optional<Error>> NewHashTreeF
     const uint64_t n = (len + (uint64_t)chunkSize - 1) / (uint64_t)chunkSize;
     std::vector<uint8_t> leaves(32 * n);
     Digest root{};
+    if (len <= kBatchLimit) {
+        auto [b, err] = Batchers::instance().get((uint64_t)chunkSize);
+        if (err) return {nullptr, err};
+        const int rc = dm_batcher_root(b, buf, len, leaves.data(), root.data());
+        if (rc == DM_ERR_EMPTY) return {nullptr, Error{rc, "Empty data"}};
+        if (rc != DM_OK) return {nullptr, Error{rc, dm_batcher_last_error()}};
+        return {build(leaves, root), std::nullopt};
+    }
     int rc = dm_root_buffer(cx.get(), buf, len, (uint64_t)chunkSize, leaves.data(), root.data());
     if (rc != DM_OK) return {nullptr, make_error(cx.get(), rc)};
     return {build(leaves, root), std::nullopt};

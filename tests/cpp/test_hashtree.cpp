@@ -3,9 +3,11 @@
 // Expected digests are computed independently with the CPU oracle's SHA-256 (linked in only as
 // the checker, never by the product library).
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "deoss_hashtree.hpp"
@@ -102,6 +104,35 @@ int main(int argc, char** argv) {
     }
     auto [sb, esb] = hashtree::Stream::New(100);
     EXPECT(!sb && esb && esb->code == DM_ERR_INVALID);
+
+    // concurrent callers (the batcher path) get the trees a single call gives
+    {
+        std::atomic<int> bad{0};
+        std::vector<std::thread> th;
+        for (int g = 0; g < 16; g++)
+            th.emplace_back([&, g] {
+                std::string b(3 * 4096 + 17 * g + 5, '\0');
+                for (size_t i = 0; i < b.size(); i++) b[i] = (char)(i * 13 + g);
+                auto [t, e] = hashtree::NewHashTreeFromBuffer(b.data(), b.size(), 4096);
+                if (e || !t) {
+                    bad++;
+                    return;
+                }
+                std::vector<hashtree::Digest> level;
+                for (size_t o = 0; o < b.size(); o += 4096) level.push_back(sha(b.substr(o, 4096)));
+                for (size_t i = 0; i < level.size(); i++)
+                    if (t->Leafs[i].Hash != level[i]) bad++;
+                do {   // merkletree v0.2.0: pair (i, i+1), the odd last node with itself
+                    std::vector<hashtree::Digest> up;
+                    for (size_t i = 0; i < level.size(); i += 2)
+                        up.push_back(sha(cat(level[i], level[std::min(i + 1, level.size() - 1)])));
+                    level = up;
+                } while (level.size() > 1);
+                if (t->MerkleRoot() != level[0]) bad++;
+            });
+        for (auto& x : th) x.join();
+        EXPECT(bad == 0);
+    }
 
     // PinnedBuffer: the same body hashed in place from page-locked memory (zero-copy path)
     auto [pb, epb] = hashtree::PinnedBuffer::New(body.size());

@@ -658,3 +658,27 @@ def test_cpp_host_mirror(tmp_path):
                     "-lpthread", "-o", exe], check=True)
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+def test_from_buffer_concurrent_batcher(oracle_lib):
+    """NewHashTreeFromBuffer from 32 threads: objects up to BATCH_LIMIT go through the process-wide
+    coalescing batcher (as in the Go package) and give the single-call trees."""
+    from deoss_amd import NewHashTreeFromBuffer
+    from deoss_amd.hashtree import _batcher
+    bodies = [oracle_lib.splitmix_bytes((3 << 20) + 4099 * g, 600 + g) for g in range(32)]
+    out = [None] * len(bodies)
+
+    def work(g):
+        out[g] = NewHashTreeFromBuffer(bodies[g], 1 << 20)
+
+    th = [threading.Thread(target=work, args=(g,)) for g in range(len(bodies))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for g, (tree, err) in enumerate(out):
+        assert err is None, g
+        lw, want = py_root_chunks(split_chunks(bodies[g], 1 << 20))
+        assert tree.MerkleRoot() == want, g
+        assert [n.Hash for n in tree.Leafs[:len(lw)]] == lw, g
+    assert _batcher(1 << 20).stats()[0] >= len(bodies)
