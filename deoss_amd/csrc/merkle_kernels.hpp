@@ -614,28 +614,45 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
 // half-rate slot).  hipcc re-associates DPP xors and cannot emit bank-masked DPP ops, so the
 // steps are written out.  Wait states: every DPP source VGPR is written at least two
 // instructions earlier.
+#ifndef DM_QS_DEEP3
+#define DM_QS_DEEP3 0
+#endif
+#if DM_QS_DEEP3
+// Experiment ("3-deep e-chain"; A/B only, tools/deep3_ab.sh): every lane of a triple
+// makes all three rotations itself (sh / sh2 / sh3 = 6,11,25 or 2,13,22) and one xor3 gives Sigma,
+// so the chain is alignbit -> xor3 -> add3 (3 deep) at 9 instructions per step instead of 8.
+#define DM_QS_HEAD(X4, X5, X6)                                                                   \
+    "v_alignbit_b32 %[r], %[" X4 "], %[" X4 "], %[sh]\n\t"                                      \
+    "v_alignbit_b32 %[s], %[" X4 "], %[" X4 "], %[sh2]\n\t"                                     \
+    "v_alignbit_b32 %[t], %[" X4 "], %[" X4 "], %[sh3]\n\t"                                     \
+    "v_bitop3_b32 %[f], %[" X4 "], %[" X5 "], %[msk] bitop3:0x1e\n\t"                          \
+    "v_bitop3_b32 %[f], %[f], %[" X6 "], %[" X5 "] bitop3:0xca\n\t"
+#define DM_QS_SIGMA "v_bitop3_b32 %[s], %[r], %[s], %[t] bitop3:0x96\n\t"
+#else
 #define DM_QS_HEAD(X4, X5, X6)                                                                   \
     "v_alignbit_b32 %[r], %[" X4 "], %[" X4 "], %[sh]\n\t"                                      \
     "v_bitop3_b32 %[f], %[" X4 "], %[" X5 "], %[msk] bitop3:0x1e\n\t"                          \
     "v_bitop3_b32 %[f], %[f], %[" X6 "], %[" X5 "] bitop3:0xca\n\t"                             \
     "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"
+#define DM_QS_SIGMA "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"
+#endif
 #define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN)                                                   \
     DM_QS_HEAD(X4, X5, X6)                                                                       \
     "v_sub_u32_dpp %[" X6 "], %[" VN "], %[" X6 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t" \
-    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    DM_QS_SIGMA                                                                                  \
     "v_sub_u32_dpp %[" HN "], %[" X4 "], %[" X6 "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
     "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
 // e-triple idle next step (steps 63, 64): keep X6 (the e-triple feeds forward from it), HN only
 // matters on the a-triple
 #define DM_QS_STEP_A(X4, X5, X6, X7, H, HN)                                                     \
     DM_QS_HEAD(X4, X5, X6)                                                                       \
-    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    DM_QS_SIGMA                                                                                  \
     "v_sub_u32_dpp %[" HN "], %[" X4 "], %[" X6 "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
     "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
 // last step of a block: no next H
 #define DM_QS_STEP_END(X4, X5, X6, X7, H)                                                       \
     DM_QS_HEAD(X4, X5, X6)                                                                       \
-    "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"        \
+    DM_QS_SIGMA                                                                                  \
     "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
 // four steps; the role registers rotate through P0..P3 = a, b, c, d and H alternates h / g
 #define DM_QS_STEPS4V(V0, V1, V2, V3)                                                          \
@@ -676,19 +693,27 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
     DM_QS_STEP_A("a", "b", "c", "d", "h", "g") DM_QS_STEP_END("d", "a", "b", "c", "g")           \
     DM_QS_FF("x0", "a", "0xc") DM_QS_FF("x1", "b", "0xc") DM_QS_FF("x3", "d", "0xc")             \
     DM_QS_FF("x2", "c", "0xc")
+#if DM_QS_DEEP3
+#define DM_QS_XOUT , [t] "=&v"(t_)
+#define DM_QS_XIN , [sh2] "v"(sh.y), [sh3] "v"(sh.z)
+#else
+#define DM_QS_XOUT
+#define DM_QS_XIN
+#endif
 #define DM_QS_OUT                                                                                \
     : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "+v"(h), [g] "+v"(g),           \
       [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),          \
-      [f] "=&v"(f_), [s] "=&v"(s_)
-#define DM_QS_OPS DM_QS_OUT : [sh] "v"(sh), [msk] "v"(msk), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3)
+      [f] "=&v"(f_), [s] "=&v"(s_) DM_QS_XOUT
+#define DM_QS_OPS DM_QS_OUT : [sh] "v"(sh.x), [msk] "v"(msk), [v0] "v"(v0), [v1] "v"(v1), [v2] "v"(v2), [v3] "v"(v3) DM_QS_XIN
 
 // One 64-byte block from the ring: 66 skewed steps (the a-triple starts two steps late and
 // finishes two steps after the e-triple).  x = this lane's chaining words: e-triple (e,f,g,h),
 // a-triple (c,d,a,b) -- stored rotated so that both triples start from P = x and feed forward
 // x += P.  kw(grp) gives -(K+W) of rounds 4grp..4grp+3 (an LDS read).
 template <class KW>
-__device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], KW kw, uint32_t sh, uint32_t msk) {
-    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h = 0, g = 0, r_, f_, s_;
+__device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], KW kw, uint3 sh, uint32_t msk) {
+    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h = 0, g = 0, r_, f_, s_, t_;
+    (void)t_;
     uint4 q = kw(0), nq = kw(1);
     {
         const uint32_t v0 = q.x, v1 = 0, v2 = 0, v3 = 0;
@@ -716,8 +741,9 @@ constexpr int kLgkmWait0 = 0xC07F;   // s_waitcnt lgkmcnt(0), no wait on vmcnt /
 // quad_block_skewed with the block's 64 words of -(K+W) in registers: the whole block is one asm
 // statement (hipcc puts an s_nop between consecutive asm statements that share registers).
 template <bool MIS>
-__device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[16], uint32_t sh, uint32_t msk) {
-    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h, g, r_, f_, s_;
+__device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[16], uint3 sh, uint32_t msk) {
+    uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h, g, r_, f_, s_, t_;
+    (void)t_;
     asm volatile(DM_QS_PROLOGUE_AT("k0", DM_QS_ALIGN_MIS)
                  DM_QS_GROUP0("k1", "k2", "k3", "k4")
                  DM_QS_STEPS4V("k5", "k6", "k7", "k8")
@@ -737,8 +763,8 @@ __device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&
                  DM_QS_TAIL("k61", "k62", "k63")
                  : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "=&v"(h), [g] "=&v"(g),
                    [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),
-                   [f] "=&v"(f_), [s] "=&v"(s_)
-                 : [mis] "i"(MIS ? 1 : 0), [sh] "v"(sh), [msk] "v"(msk),
+                   [f] "=&v"(f_), [s] "=&v"(s_) DM_QS_XOUT
+                 : [mis] "i"(MIS ? 1 : 0), [sh] "v"(sh.x), [msk] "v"(msk),
                    [k0] "v"(K[0].x), [k1] "v"(K[0].y), [k2] "v"(K[0].z), [k3] "v"(K[0].w),
                    [k4] "v"(K[1].x), [k5] "v"(K[1].y), [k6] "v"(K[1].z), [k7] "v"(K[1].w),
                    [k8] "v"(K[2].x), [k9] "v"(K[2].y), [k10] "v"(K[2].z), [k11] "v"(K[2].w),
@@ -754,14 +780,14 @@ __device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&
                    [k48] "v"(K[12].x), [k49] "v"(K[12].y), [k50] "v"(K[12].z), [k51] "v"(K[12].w),
                    [k52] "v"(K[13].x), [k53] "v"(K[13].y), [k54] "v"(K[13].z), [k55] "v"(K[13].w),
                    [k56] "v"(K[14].x), [k57] "v"(K[14].y), [k58] "v"(K[14].z), [k59] "v"(K[14].w),
-                   [k60] "v"(K[15].x), [k61] "v"(K[15].y), [k62] "v"(K[15].z), [k63] "v"(K[15].w));
+                   [k60] "v"(K[15].x), [k61] "v"(K[15].y), [k62] "v"(K[15].z), [k63] "v"(K[15].w) DM_QS_XIN);
 }
 
 // One ring stage (8 blocks) when every leaf of the wave has all 8: each block's 64 K+W words go
 // to registers in one burst while the previous block runs (one s_waitcnt per block instead of
 // one per 4 rounds), and no per-block branch.
 template <int G, int ROW, bool MIS>
-__device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* kw, uint32_t sh, uint32_t msk) {
+__device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* kw, uint3 sh, uint32_t msk) {
     uint4 A[16], B[16];
 #pragma unroll
     for (int g = 0; g < 16; g++) A[g] = kw[g * G];
@@ -844,7 +870,11 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         const uint32_t p = lane & 3;
         const uint64_t iq = first + cq;
         const LeafView vq = leaf_view<TABLE>(a, iq);
-        const uint32_t sh = role_a ? (p == 0 ? 2 : p == 1 ? 13 : 22) : (p == 0 ? 6 : p == 1 ? 11 : 25);
+#if DM_QS_DEEP3
+        const uint3 sh = role_a ? make_uint3(2, 13, 22) : make_uint3(6, 11, 25);
+#else
+        const uint3 sh = make_uint3(role_a ? (p == 0 ? 2 : p == 1 ? 13 : 22) : (p == 0 ? 6 : p == 1 ? 11 : 25), 0, 0);
+#endif
         const uint32_t msk = role_a ? 0u : ~0u;
         uint32_t st0[8];
         if (vq.active) load_or_init_state(a, iq, st0);
