@@ -13,6 +13,7 @@ a chunk-size sweep and the host-buffer end-to-end rate.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -92,7 +93,7 @@ def main() -> None:
                          "(other_configs), the e2e host-buffer rates and the 64 KiB / 1 MiB sweep points")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--workload", default="object",
-                    choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files",
+                    choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files", "fullprocessing",
                              "plumbing"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
@@ -143,7 +144,7 @@ def main() -> None:
 
     runners = {"upload": run_upload, "files": run_files, "plumbing": run_plumbing, "rs": run_rs,
                "process": run_process, "proofs": run_proofs, "concurrent": run_concurrent,
-               "batch": run_batch, "stream": run_batch}
+               "batch": run_batch, "stream": run_batch, "fullprocessing": run_fullprocessing}
     if args.workload in runners:
         res = runners[args.workload](args, torch, dist, world, rank, device, dev_index, gloo)
         if res is not None and rank == 0:
@@ -440,6 +441,8 @@ def driver_extras(args, torch, dist, device, dev_index):
                                                        warmup=1)),
         ("FullProcessing", run_process, dict(workload="process", object_gib=8.0, steps=2, warmup=1, no_cpu=True)),
         ("reed_solomon_4+8", run_rs, dict(workload="rs", object_gib=8.0, steps=3, warmup=1, no_cpu=True)),
+        ("FullProcessing_file", run_fullprocessing, dict(workload="fullprocessing", object_gib=2.0, steps=2,
+                                                         warmup=1, no_cpu=True)),
     ]
     res = {}
     for name, fn, kw in specs:
@@ -914,6 +917,145 @@ def run_process(args, torch, dist, world, rank, device, dev_index, gloo):
                                "kind": "port", "sample": f"{sample} segments x {seg} B of the same object through "
                                "oracle/process_oracle.c (SHA-NI SHA-256 + table GF(2^8) RS, serial like the SDK)"}
     return out
+
+
+def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #2 end to end, as every upload handler calls it: FullProcessing(file, "", savedir) on a
+    --object-gib file in /dev/shm (page cache) -> fragment and segment files in savedir, fid.  One
+    step = one dm_full_processing call (pread into pinned slots, H2D, data-fragment writes while
+    reading, one RS + one leaf launch, parity back and written while the leaf chains run, renames).
+    Beside it, untimed for the value: the window path (read 8 segments, one dm_process_buffer
+    call, write their fragments from Python, repeat: serial, the Python mirror's earlier shape) and
+    the same file I/O done from Python alone (read the file, write the same bytes as 8 MiB / 32 MiB
+    files, 16 threads, no hashing or coding).
+    savedir is emptied (untimed) before every run, so every run writes every file."""
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from deoss_amd import MerkleContext
+    from deoss_amd.process import Processor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    seg, k, m = 32 << 20, 4, 8
+    frag, total = seg // k, k + m
+    length = int(args.object_gib * (1 << 30))
+    nseg = -(-length // seg)
+    out_bytes = nseg * (total * frag + seg)               # fragments + segment files
+    orc = Oracle()
+    need = length + out_bytes + (1 << 30)
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > need else None
+    d = tempfile.mkdtemp(prefix="deoss_fp_", dir=base)
+    try:
+        path = os.path.join(d, "object.bin")
+        piece = torch.empty(64 << 20, dtype=torch.uint8)
+        with open(path, "wb") as f:
+            for off in range(0, length, 64 << 20):
+                n = min(64 << 20, length - off)
+                orc.fill_splitmix_ptr(piece.data_ptr(), off, (n + 7) // 8 * 8, SEED + 0x300)
+                f.write(piece.numpy()[:n].tobytes())
+        del piece
+        ctx = MerkleContext(devices=[dev_index])
+        proc = Processor(ctx, k, m, seg)
+        savedir = os.path.join(d, "cache")
+
+        def fresh():
+            shutil.rmtree(savedir, ignore_errors=True)
+
+        for _ in range(args.warmup):
+            fresh()
+            proc.full_processing_file(path, savedir)
+        times = []
+        ctx.set_timing(True)
+        for _ in range(args.steps):
+            fresh()
+            t0 = time.perf_counter()
+            segd, fragd, fid = proc.full_processing_file(path, savedir)
+            times.append(time.perf_counter() - t0)
+        n_t, k_sum, _, _ = ctx.timing_summary()
+        ctx.set_timing(False)
+        tavg = sum(times) / len(times)
+        # parity: every segment digest + fid against the CPU restatement over the same bytes, all
+        # fragment digests of the first and last segment, the files on disk (names = SHA-256 of
+        # their bytes for a sample, exactly the expected set, no temporary left)
+        import numpy as np
+        host = np.fromfile(path, dtype=np.uint8)
+        threads = min(16, os.cpu_count() or 1)
+        padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
+        want_seg = orc.root_buffer_ptr(host.ctypes.data, (nseg - 1) * seg, seg, threads, True)[0] if nseg > 1 else b""
+        want_seg = (want_seg or b"") + orc.sha256(padded)
+        frag_ok = True
+        for s_i in sorted({0, nseg - 1}):
+            sbytes = padded if s_i == nseg - 1 else host[s_i * seg:(s_i + 1) * seg].tobytes()
+            frag_ok &= orc.full_processing(sbytes, seg, k, m, nthreads=threads)[1] == \
+                fragd[s_i * total * 32:(s_i + 1) * total * 32]
+        del host
+        names = set(os.listdir(savedir))
+        expect = {fragd[32 * t:32 * t + 32].hex() for t in range(nseg * total)} | \
+                 {segd[32 * t:32 * t + 32].hex() for t in range(nseg)}
+        sample = sorted(expect)[:8]
+        files_ok = names == expect and all(
+            hashlib.sha256(open(os.path.join(savedir, n), "rb").read()).hexdigest() == n for n in sample)
+        parity = {"fid": fid.hex(), "segment_digests": nseg, "fragment_digests_checked_segments": sorted({0, nseg - 1}),
+                  "files_on_disk": len(names), "files_expected": len(expect), "files_hash_checked": len(sample),
+                  "bit_exact": bool(segd == want_seg and fid == orc.reduce(want_seg)[:32] and frag_ok and files_ok)}
+        # the window path, same file, same savedir state
+        fresh()
+        t0 = time.perf_counter()
+        info, wfid, err = proc.FullProcessingWindows(path, "", savedir)
+        t_win = time.perf_counter() - t0
+        parity["window_path_fid_equal"] = err is None and wfid == fid.hex()
+        # the same file I/O from Python alone: read the file, write the same output bytes as files
+        fresh()
+        os.makedirs(savedir)
+        t0 = time.perf_counter()
+
+        def rd(off):
+            with open(path, "rb") as f:
+                f.seek(off)
+                return f.read(min(64 << 20, length - off))
+
+        def wr(i):
+            src = blob[(i % (len(blob) // frag)) * frag:][:frag] if i < nseg * total else blob[:seg]   # views
+            with open(os.path.join(savedir, f"io{i}"), "wb") as f:
+                f.write(src)
+
+        with ThreadPoolExecutor(16) as ex:
+            blob = memoryview(b"".join(ex.map(rd, range(0, min(length, 256 << 20), 64 << 20))))
+            list(ex.map(rd, range(256 << 20, length, 64 << 20)))
+            list(ex.map(wr, range(nseg * total + nseg)))
+        t_io = time.perf_counter() - t0
+        fresh()
+        k_avg = k_sum / max(n_t, 1)
+        out = {
+            "metric": "GiB/s of a file through FullProcessing(file, \"\", savedir): file -> fragment + segment files, fid",
+            "value": round(length / tavg / (1 << 30), 4), "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(tavg * 1e3, 3), "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": "u32 (SHA-256), u8 (GF(2^8))",
+            "data": f"synthetic splitmix64 file in {'/dev/shm' if base else 'the temp dir'}",
+            "config": {"workload": f"1 file of {length} B -> {nseg} segments of {seg} B -> {k}+{m} fragments of "
+                                   f"{frag} B; writes {out_bytes} B ({nseg * total} fragment + {nseg} segment files)",
+                       "object_bytes": length, "output_bytes": out_bytes},
+            "step_ms": [round(t * 1e3, 1) for t in times],
+            "leaf_kernel_avg_ms": round(k_avg, 3),
+            "window_path": {"GiBps": round(length / t_win / (1 << 30), 4), "ms": round(t_win * 1e3, 1),
+                            "what": "read 8 segments, dm_process_buffer, write their files from Python, repeat"},
+            "python_io_only": {"GiBps": round(length / t_io / (1 << 30), 4), "ms": round(t_io * 1e3, 1),
+                               "what": f"read {length} B + write {out_bytes} B as the same number of files from "
+                                       "Python, 16 threads, no hashing or coding (a host-side reference point)"},
+            "parity": parity,
+        }
+        if not args.no_cpu:
+            sample_n = min(nseg, 2)
+            buf = open(path, "rb").read(sample_n * seg)
+            t0 = time.perf_counter()
+            orc.full_processing(buf, seg, k, m, nthreads=1)
+            dt = time.perf_counter() - t0
+            out["cpu_baseline"] = {"value": round(len(buf) / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
+                                   "kind": "port", "sample": f"{sample_n} segments of the same file through "
+                                   "oracle/process_oracle.c (SHA-256 + RS, serial like the SDK; no file writes)"}
+        return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):

@@ -1,0 +1,296 @@
+// fullproc_capi.inl -- dm_full_processing: cess-go-sdk process.FullProcessing(file, "", savedir)
+// (go.mod:8; called at node/objectHandler.go:168, node/fileHandler.go:771,
+// node/filesHandler.go:201, node/resumeHandler.go:326, node/tracker.go:767-769) from the file path,
+// in one call.  Part of merkle_capi.hip (after files_capi.inl, rs_capi.inl, process_capi.inl).
+//
+// Per window of segments (up to kFpWindowBytes of file; one window up to 32 GiB):
+//   A. the file is pread into pinned slots (whole segments per slot, parallel readers); each slot
+//      is copied to HBM, and its data fragments -- plain file bytes, so their contents are known
+//      already -- are written to temporary files by background writers while the next slot is
+//      read (the last segment's zero padding is filled in the slot);
+//   B. one RS launch and one leaf launch over the window's segments and fragments
+//      (process_segments, the same GPU pass as dm_process_buffer);
+//   C. while the leaf kernel's serial chains run (~0.5 s for 32 MiB segments), the parity
+//      fragments come back through the same slots and are written to temporary files;
+//   D. the digests come back and every temporary file is renamed to savedir/<hex SHA-256>.
+// The fid is the hashtree root over all segment digests.  The Go shim's window path (read a
+// window, one batched GPU call, then write its fragments) leaves the GPU idle during the writes
+// and the writes idle during the hashing; here they overlap.
+
+namespace {
+
+constexpr uint64_t kFpSlotBytes = 64ull << 20;         // pinned slot (whole segments / parity sets)
+constexpr int kFpSlots = 4;                             // = dm_rs::fp_slot
+constexpr int kFpWritersPerSlot = 4;                    // background write jobs per slot
+constexpr uint64_t kFpWindowBytes = 32ull << 30;        // file bytes per GPU pass (+ 2x parity in HBM)
+
+std::atomic<uint64_t> g_fp_seq{0};
+
+uint64_t env_bytes(const char* name, uint64_t dflt) {
+    const char* v = std::getenv(name);
+    const unsigned long long x = v ? std::strtoull(v, nullptr, 10) : 0;
+    return x ? (uint64_t)x : dflt;
+}
+
+std::string hex32(const uint8_t* d) {
+    static const char* x = "0123456789abcdef";
+    std::string s(64, '0');
+    for (int i = 0; i < 32; i++) {
+        s[2 * i] = x[d[i] >> 4];
+        s[2 * i + 1] = x[d[i] & 15];
+    }
+    return s;
+}
+
+// os.WriteFile(path, data, os.ModePerm), as the Go shim writes fragments; "" on success.
+std::string write_whole(const std::string& path, const uint8_t* p, uint64_t len) {
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0777);
+    if (fd < 0) return "open " + path + ": " + go_errno(errno);
+    uint64_t done = 0;
+    while (done < len) {
+        const ssize_t w = ::write(fd, p + done, len - done);
+        if (w < 0 && errno == EINTR) continue;
+        if (w <= 0) {
+            const int e = w < 0 ? errno : EIO;
+            ::close(fd);
+            return "write " + path + ": " + go_errno(e);
+        }
+        done += (uint64_t)w;
+    }
+    if (::close(fd) != 0) return "close " + path + ": " + go_errno(errno);
+    return "";
+}
+
+// os.MkdirAll(dir, 0755)
+std::string mkdir_all(const std::string& dir) {
+    for (size_t i = 1; i <= dir.size(); i++) {
+        if (i < dir.size() && dir[i] != '/') continue;
+        const std::string p = dir.substr(0, i);
+        struct stat st {};
+        if (::stat(p.c_str(), &st) == 0) {
+            if (!S_ISDIR(st.st_mode)) return "mkdir " + p + ": not a directory";
+            continue;
+        }
+        if (::mkdir(p.c_str(), 0755) != 0 && errno != EEXIST) return "mkdir " + p + ": " + go_errno(errno);
+    }
+    return "";
+}
+
+struct FpFile {          // one file to write: bytes, temporary name, and where its digest will be
+    const uint8_t* src;
+    uint64_t len;
+    std::string tmp;
+};
+
+// Background writes out of one pinned slot; wait() joins them before the slot is refilled.
+struct SlotWrites {
+    std::vector<std::future<std::string>> jobs;
+    void start(std::vector<FpFile> files) {
+        const size_t J = std::min<size_t>(kFpWritersPerSlot, files.size());
+        for (size_t j = 0; j < J; j++) {
+            std::vector<FpFile> mine;
+            for (size_t i = j; i < files.size(); i += J) mine.push_back(files[i]);
+            jobs.push_back(std::async(std::launch::async, [mine]() {
+                for (const auto& f : mine) {
+                    std::string e = write_whole(f.tmp, f.src, f.len);
+                    if (!e.empty()) return e;
+                }
+                return std::string();
+            }));
+        }
+    }
+    std::string wait() {   // first error, once every job has finished
+        std::string err;
+        for (auto& j : jobs) {
+            std::string e = j.get();
+            if (err.empty()) err = e;
+        }
+        jobs.clear();
+        return err;
+    }
+    ~SlotWrites() { (void)wait(); }
+};
+
+struct FpEvents {
+    hipEvent_t slot[kFpSlots] = {}, rs = nullptr, copied = nullptr;
+    ~FpEvents() {
+        for (hipEvent_t e : slot)
+            if (e) (void)hipEventDestroy(e);
+        if (rs) (void)hipEventDestroy(rs);
+        if (copied) (void)hipEventDestroy(copied);
+    }
+};
+
+// Everything but the renames; `pend` collects (temporary name, digest slot) of every file written.
+int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir, uint64_t seg, int flags,
+                            std::vector<uint8_t>& segd, std::vector<uint8_t>& fragd,
+                            std::vector<std::pair<std::string, uint64_t>>& pend, uint8_t fid[32]) {
+    dm_ctx* c = r->c;
+    Dev& d = c->devs[0];
+    hipStream_t s = d.stream;
+    const int k = r->k, m = r->m, total = k + m;
+    const uint64_t frag = seg / (uint64_t)k, pbytes = (uint64_t)m * frag;   // parity bytes per segment
+    const uint64_t size = fs.size[0], nseg = ceil_div(size, seg);
+    // test hooks (env, read per call): smaller slots / windows exercise slot reuse and multi-window fids
+    const uint64_t slot_bytes = env_bytes("DEOSS_FP_SLOT_BYTES", kFpSlotBytes);
+    const uint64_t window_bytes = env_bytes("DEOSS_FP_WINDOW_BYTES", kFpWindowBytes);
+    const uint64_t spd = std::max<uint64_t>(1, slot_bytes / seg);            // segments per data slot
+    const uint64_t spp = std::max<uint64_t>(1, slot_bytes / pbytes);         // segments per parity slot
+    const uint64_t slot_cap = std::max(spd * seg, spp * pbytes);
+    const uint64_t win = std::max<uint64_t>(spd, window_bytes / seg / spd * spd);   // segments per window
+    RC_TRY(begin_call(c, d, s));
+    for (auto& b : r->fp_slot) HIP_TRY(b.ensure(slot_cap));
+    FpEvents ev;
+    for (auto& e : ev.slot) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ev.rs, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&ev.copied, hipEventDisableTiming));
+    const std::string base = dir + "/.dm-fp-" + std::to_string((long long)::getpid()) + "-" +
+                             std::to_string((unsigned long long)g_fp_seq++) + "-";
+    SlotWrites wr[kFpSlots];
+    bool busy[kFpSlots] = {false, false, false, false};
+    uint64_t next = 0;   // slot round robin across both phases and windows
+    auto take_slot = [&](int* out) -> int {
+        const int sl = (int)(next++ % kFpSlots);
+        if (busy[sl]) {
+            HIP_TRY(hipEventSynchronize(ev.slot[sl]));
+            const std::string e = wr[sl].wait();
+            if (!e.empty()) return fail(c, DM_ERR_IO, "%s", e.c_str());
+            busy[sl] = false;
+        }
+        *out = sl;
+        return DM_OK;
+    };
+    const bool one_window = nseg <= win;
+    for (uint64_t w0 = 0; w0 < nseg; w0 += win) {
+        const uint64_t ns = std::min(win, nseg - w0);
+        const uint64_t fbeg = w0 * seg, fend = std::min(size, (w0 + ns) * seg);
+        HIP_TRY(d.data.ensure(ns * seg + kAlign));
+        HIP_TRY(r->work.ensure(ns * pbytes + 32));
+        uint8_t* parity = r->work.u8();
+        uint8_t* dfid = parity + ns * pbytes;
+        // A: file -> slots -> HBM; data fragments (+ segments) written from the slot meanwhile
+        for (uint64_t t0 = 0; t0 < ns; t0 += spd) {
+            const uint64_t nt = std::min(spd, ns - t0), len = nt * seg, a = fbeg + t0 * seg;
+            int sl;
+            RC_TRY(take_slot(&sl));
+            uint8_t* buf = r->fp_slot[sl].u8();
+            const uint64_t have = a < fend ? std::min(len, fend - a) : 0;
+            std::vector<FilePart> parts;
+            for (uint64_t q = 0; q < have; q += 16ull << 20)
+                parts.push_back({0, a + q, std::min<uint64_t>(16ull << 20, have - q), buf + q});
+            RC_TRY(read_parts(c, fs, parts));
+            if (have < len) std::memset(buf + have, 0, len - have);
+            HIP_TRY(hipMemcpyAsync(d.data.u8() + t0 * seg, buf, len, hipMemcpyHostToDevice, d.copy));
+            HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
+            std::vector<FpFile> files;
+            for (uint64_t u = 0; u < nt; u++) {
+                const uint64_t gs = w0 + t0 + u;
+                for (int j = 0; j < k; j++) {
+                    const uint64_t id = gs * (uint64_t)total + (uint64_t)j;
+                    files.push_back({buf + u * seg + (uint64_t)j * frag, frag, base + "f" + std::to_string(id)});
+                    pend.emplace_back(files.back().tmp, 32 * id);
+                }
+                if (flags & DM_FP_SEGMENT_FILES) {
+                    files.push_back({buf + u * seg, seg, base + "s" + std::to_string(gs)});
+                    pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
+                }
+            }
+            wr[sl].start(std::move(files));
+            busy[sl] = true;
+        }
+        // B: RS + one leaf launch over segments and fragments, after the last H2D
+        HIP_TRY(hipEventRecord(ev.copied, d.copy));
+        HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
+        RC_TRY(process_segments(r, d, s, d.data.u8(), seg, parity, {0, ns}, dfid, ev.rs));
+        // C: parity back through the slots while the leaf chains run; written as each set lands
+        HIP_TRY(hipStreamWaitEvent(d.copy, ev.rs, 0));
+        for (uint64_t t0 = 0; t0 < ns; t0 += spp) {
+            const uint64_t nt = std::min(spp, ns - t0);
+            int sl;
+            RC_TRY(take_slot(&sl));
+            uint8_t* buf = r->fp_slot[sl].u8();
+            HIP_TRY(hipMemcpyAsync(buf, parity + t0 * pbytes, nt * pbytes, hipMemcpyDeviceToHost, d.copy));
+            HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
+            HIP_TRY(hipEventSynchronize(ev.slot[sl]));
+            std::vector<FpFile> files;
+            for (uint64_t u = 0; u < nt; u++) {
+                const uint64_t gs = w0 + t0 + u;
+                for (int i = 0; i < m; i++) {
+                    const uint64_t id = gs * (uint64_t)total + (uint64_t)(k + i);
+                    files.push_back({buf + u * pbytes + (uint64_t)i * frag, frag, base + "f" + std::to_string(id)});
+                    pend.emplace_back(files.back().tmp, 32 * id);
+                }
+            }
+            wr[sl].start(std::move(files));
+            busy[sl] = true;
+        }
+        // D: digests (d.leaves: segment t at t, fragment (t, j) at ns + t * total + j)
+        HIP_TRY(hipMemcpyAsync(segd.data() + 32 * w0, d.leaves.p, 32 * ns, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(fragd.data() + 32 * w0 * total, d.leaves.u8() + 32 * ns, 32 * ns * total,
+                               hipMemcpyDeviceToHost, s));
+        if (one_window) HIP_TRY(hipMemcpyAsync(fid, dfid, 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipStreamSynchronize(d.copy));   // this window's slots are in host memory: HBM reusable
+    }
+    for (int sl = 0; sl < kFpSlots; sl++) {
+        const std::string e = wr[sl].wait();
+        if (!e.empty()) return fail(c, DM_ERR_IO, "%s", e.c_str());
+    }
+    if (!one_window) {   // several windows: the fid is the tree over every segment digest
+        HIP_TRY(d.leaves.ensure(32 * nseg));
+        HIP_TRY(hipMemcpyAsync(d.leaves.p, segd.data(), 32 * nseg, hipMemcpyHostToDevice, s));
+        RC_TRY(finish(c, d, s, d.leaves.u8(), nseg, true, d.root.u8()));
+        HIP_TRY(hipMemcpyAsync(fid, d.root.p, 32, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    return DM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t segment, int flags,
+                       uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out, uint8_t fid[32]) {
+    if (!r || !path || !savedir || !fid) return bad_arg();
+    dm_ctx* c = r->c;
+    CallLock lk(c->mu);
+    if (nseg_out) *nseg_out = 0;
+    FileSet fs;
+    RC_TRY(open_files(c, &path, 1, fs));   // "open <path>: ..." first, as os.Open would fail
+    const uint64_t size = fs.size[0];
+    if (size == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
+    RC_TRY(process_check(r, size, segment));
+    const uint64_t nseg = ceil_div(size, segment);
+    if (nseg_out) *nseg_out = nseg;
+    if ((seg_hashes || frag_hashes) && cap < nseg)
+        return fail(c, DM_ERR_INVALID, "dm_full_processing: %llu segments, digest arrays hold %llu",
+                    (unsigned long long)nseg, (unsigned long long)cap);
+    std::string dir = savedir;
+    while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
+    const std::string me = mkdir_all(dir);
+    if (!me.empty()) return fail(c, DM_ERR_IO, "%s", me.c_str());
+    const int total = r->k + r->m;
+    std::vector<uint8_t> segd(32 * nseg), fragd(32 * nseg * total);
+    std::vector<std::pair<std::string, uint64_t>> pend;
+    int rc = full_processing_windows(r, fs, dir, segment, flags, segd, fragd, pend, fid);
+    for (size_t i = 0; rc == DM_OK && i < pend.size(); i++) {
+        const uint64_t at = pend[i].second;
+        const uint8_t* dig = (at >> 63) ? segd.data() + ~at : fragd.data() + at;
+        const std::string to = dir + "/" + hex32(dig);
+        if (::rename(pend[i].first.c_str(), to.c_str()) != 0)
+            rc = fail(c, DM_ERR_IO, "rename %s %s: %s", pend[i].first.c_str(), to.c_str(), go_errno(errno).c_str());
+        else
+            pend[i].first.clear();
+    }
+    if (rc != DM_OK) {   // no temporary survives a failed call
+        for (const auto& p : pend)
+            if (!p.first.empty()) ::unlink(p.first.c_str());
+        return rc;
+    }
+    if (seg_hashes) std::memcpy(seg_hashes, segd.data(), segd.size());
+    if (frag_hashes) std::memcpy(frag_hashes, fragd.data(), fragd.size());
+    return DM_OK;
+}
+
+}  // extern "C"

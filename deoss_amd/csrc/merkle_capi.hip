@@ -14,12 +14,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1197,5 +1199,6 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
 #include "files_capi.inl"
 #include "rs_capi.inl"
 #include "process_capi.inl"
+#include "fullproc_capi.inl"
 #include "tree_capi.inl"
 #include "batcher.inl"

@@ -19,9 +19,10 @@ namespace {
 // nseg segments at `obj` (segment-contiguous, padding already zeroed) belonging to objects whose
 // segments start at first[o] (first.size() == nobj + 1): RS coding, one leaf launch over every
 // segment and fragment, one fid per object into fids (nobj x 32, device).  Digests land in
-// d.leaves: segment s at s, fragment (s, j) at nseg + s * total + j.
+// d.leaves: segment s at s, fragment (s, j) at nseg + s * total + j.  after_rs (nullable) is
+// recorded once the parity is written, so a caller can copy it out while the leaf kernel runs.
 int process_segments(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t segment, uint8_t* parity,
-                     const std::vector<uint64_t>& first, uint8_t* fids) {
+                     const std::vector<uint64_t>& first, uint8_t* fids, hipEvent_t after_rs = nullptr) {
     dm_ctx* c = r->c;
     const int k = r->k, m = r->m, total = k + m;
     const uint64_t nseg = first.back(), frag = segment / (uint64_t)k, nobj = first.size() - 1;
@@ -36,6 +37,7 @@ int process_segments(dm_rs* r, Dev& d, hipStream_t s, uint8_t* obj, uint64_t seg
     a.nout = (uint32_t)m;
     launch_rs(d, s, k, a);
     HIP_TRY(hipGetLastError());
+    if (after_rs) HIP_TRY(hipEventRecord(after_rs, s));
     // leaf table: segments first (their chains are the longest: they start first), then fragments
     const uint64_t T = nseg * (1 + (uint64_t)total);
     std::vector<uint64_t> addr(T), lens(T);

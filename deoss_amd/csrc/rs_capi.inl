@@ -88,6 +88,7 @@ struct dm_rs {
     DevBuf enc_tab;             // parity rows, k x 256 x 8 B
     DevBuf dec_tab;             // per reconstruct call
     DevBuf work;                // host-API shard staging
+    PinnedBuf fp_slot[4];       // dm_full_processing: file / parity slots (fullproc_capi.inl)
 };
 
 namespace {
@@ -224,6 +225,7 @@ void dm_rs_destroy(dm_rs* r) {
         r->enc_tab.release();
         r->dec_tab.release();
         r->work.release();
+        for (auto& b : r->fp_slot) b.release();
     }
     delete r;
 }

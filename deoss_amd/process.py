@@ -18,6 +18,8 @@ from cess-go-sdk (``go.mod:8``; not vendored): ``node/objectHandler.go:168``,
 
 Coding, hashing and the tree run on the GPU; there is no CPU fallback.  Segment files are written
 too (the zero-padded segment = its data fragments in order), so every returned path exists.
+:meth:`Processor.FullProcessing` is one ``dm_full_processing`` call: the library reads the file,
+and fragment writes overlap the reads and the GPU's hashing.
 Deviation: a non-empty ``cipher`` is rejected (the AES branch is not implemented).
 """
 from __future__ import annotations
@@ -27,7 +29,7 @@ import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
-from ._lib import DM_ERR_EMPTY, DM_ERR_INVALID, DeossMerkleError
+from ._lib import DM_ERR_EMPTY, DM_ERR_INVALID, DM_ERR_IO, DeossMerkleError
 from .merkle import MerkleContext
 from .reedsolomon import DATA_SHARDS, PAR_SHARDS, Encoder
 
@@ -125,8 +127,57 @@ class Processor:
                                                         stream), "dm_process_device_async")
 
     # -- FullProcessing ----------------------------------------------------------------------------
+    def full_processing_file(self, file: str, savedir: str, segment_files: bool = True
+                             ) -> Tuple[bytes, bytes, bytes]:
+        """One ``dm_full_processing`` call: the library reads ``file``, writes every fragment (and
+        segment) to ``savedir/<hex SHA-256>`` and returns (segment digests, fragment digests, fid)."""
+        L = self.ctx._L
+        try:
+            size = os.stat(file).st_size
+        except OSError:
+            size = 0
+        cap = max(1, (size + self.segment - 1) // self.segment)
+        total = self.k + self.m
+        for _ in range(2):   # a FIFO / a file that grew: retry once with the count the library saw
+            seg = ctypes.create_string_buffer(32 * cap)
+            frag = ctypes.create_string_buffer(32 * cap * total)
+            fid = ctypes.create_string_buffer(32)
+            nseg = ctypes.c_uint64(0)
+            rc = L.dm_full_processing(self.enc._h, os.fsencode(file), os.fsencode(savedir), self.segment,
+                                      1 if segment_files else 0, seg, frag, cap, ctypes.byref(nseg), fid)
+            if rc == DM_ERR_INVALID and nseg.value > cap:
+                cap = nseg.value
+                continue
+            if rc == DM_ERR_IO:   # file errors keep Go's text ("open <path>: no such file or directory")
+                raise DeossMerkleError(rc, (L.dm_last_error(None) or b"").decode())
+            self._check(rc, "dm_full_processing")
+            n = nseg.value
+            return seg.raw[:32 * n], frag.raw[:32 * n * total], fid.raw
+        raise DeossMerkleError(DM_ERR_INVALID, "dm_full_processing: file size changed during the call")
+
     def FullProcessing(self, file: str, cipher: str, savedir: str
                        ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
+        """FullProcessing in one library call (``dm_full_processing``: reads, coding, hashing and
+        fragment writes overlapped)."""
+        if cipher:
+            return None, "", DeossMerkleError(DM_ERR_INVALID, "cipher is not supported by the GPU pipeline")
+        try:
+            segd, fragd, fid = self.full_processing_file(file, savedir)
+        except (OSError, DeossMerkleError) as e:
+            return None, "", e
+        total = self.k + self.m
+        info = []
+        for s in range(len(segd) // 32):
+            names = [os.path.join(savedir, fragd[32 * (s * total + j):32 * (s * total + j + 1)].hex())
+                     for j in range(total)]
+            info.append(SegmentDataInfo(os.path.join(savedir, segd[32 * s:32 * s + 32].hex()), names))
+        return info, fid.hex(), None
+
+    def FullProcessingWindows(self, file: str, cipher: str, savedir: str
+                              ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
+        """The window path (the Go shim's shape before dm_full_processing): read a window of
+        ``WINDOW_SEGMENTS`` segments, one ``dm_process_buffer`` call, write its fragments, repeat.
+        Kept as the A/B baseline of ``bench.py --workload fullprocessing``."""
         if cipher:
             return None, "", DeossMerkleError(DM_ERR_INVALID, "cipher is not supported by the GPU pipeline")
         try:

@@ -7,10 +7,12 @@
 // (node/fileHandler.go:964,997).  Same signature and result shape; segmenting, Reed-Solomon 4 + 8
 // coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h): calls
 // from concurrent handler goroutines go through one dm_batcher, which coalesces whatever is
-// queued into one batched GPU pass (dm_batcher_process), and dm_tree_levels builds the fid of
-// files larger than one window.  Go memory is bounded process-wide: 1 GiB per window of 8
-// segments in flight, DEOSS_PROCESS_MEM_GIB (default 8) windows at once across every upload,
-// buffers pooled, fragments written to disk as each window completes.  Swap it in by changing the handlers' import of
+// queued into one batched GPU pass (dm_batcher_process); files larger than one window (8
+// segments) go through dm_full_processing on a per-GPU pipeline, which reads the file, writes
+// every fragment and segment file itself and overlaps those writes with the GPU's coding and
+// hashing (one GPU pass per 32 GiB of file, no Go memory for the data).  Go memory of the small
+// path is bounded process-wide: 1 GiB per window in flight, DEOSS_PROCESS_MEM_GIB (default 8)
+// windows at once across every upload, buffers pooled.  Swap it in by changing the handlers' import of
 // github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
 // Deviation: cipher must be "" (the AES branch is not implemented; INTEGRATION.md).  Segment and
 // fragment files are both written to savedir under their hex SHA-256.  Build with `-tags hip`,
@@ -52,6 +54,7 @@ var (
 	initEr  error
 	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
 	bufs    sync.Pool     // *windowBuf, reused across calls
+	pipes   chan *C.dm_rs // large files: one dm_full_processing pipeline per GPU
 	// writeSegments: SegmentHash paths exist as files (the zero-padded segment bytes), like the
 	// fragment paths; DEOSS_SKIP_SEGMENT_FILES=1 skips them (DeOSS itself only opens fragments).
 	writeSegments = os.Getenv("DEOSS_SKIP_SEGMENT_FILES") != "1"
@@ -77,6 +80,22 @@ func gpu() error {
 		if rc := C.dm_create(&ctx, nil, 0); rc != C.DM_OK {
 			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
 			return
+		}
+		ngpu := int(C.dm_gpu_count())
+		pipes = make(chan *C.dm_rs, ngpu)
+		for g := 0; g < ngpu; g++ {
+			var pc *C.dm_ctx
+			var rs *C.dm_rs
+			dev := C.int(g)
+			if rc := C.dm_create(&pc, &dev, 1); rc != C.DM_OK {
+				initEr = errors.New(C.GoString(C.dm_strerror(rc)))
+				return
+			}
+			if rc := C.dm_rs_create(pc, C.int(chain.DataShards), C.int(chain.ParShards), &rs); rc != C.DM_OK {
+				initEr = errors.New(C.GoString(C.dm_strerror(rc)))
+				return
+			}
+			pipes <- rs
 		}
 		// every visible GPU, 2 worker slots each, 4096 leaves per batch, 2 ms linger (DESIGN.md §6.9)
 		if rc := C.dm_batcher_create(nil, 0, C.DM_BATCH_PROCESS, C.uint64_t(chain.SegmentSize), C.int(chain.DataShards),
@@ -193,6 +212,9 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 	seg := uint64(chain.SegmentSize)
 	total := chain.DataShards + chain.ParShards
 	nsegAll := (size + seg - 1) / seg
+	if nsegAll > windowSegments {
+		return fullProcessingLarge(file, savedir, nsegAll)
+	}
 	var wins []*window
 	for first := uint64(0); first < nsegAll; first += windowSegments {
 		nseg := min(uint64(windowSegments), nsegAll-first)
@@ -251,4 +273,60 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		copy(fid[:], nodes[len(nodes)-32:])
 	}
 	return info, hex.EncodeToString(fid[:]), nil
+}
+
+// fullProcessingLarge: one dm_full_processing call on a free per-GPU pipeline.  The library reads
+// the file, writes every fragment and segment file to savedir/<hex SHA-256> (data fragments while
+// the file is still being read, parity fragments while the leaf kernel hashes) and returns the
+// digests and the fid.
+func fullProcessingLarge(file, savedir string, nseg uint64) ([]chain.SegmentDataInfo, string, error) {
+	total := uint64(chain.DataShards + chain.ParShards)
+	rs := <-pipes
+	defer func() { pipes <- rs }()
+	for attempt := 0; ; attempt++ {
+		segd := make([]byte, 32*nseg)
+		fragd := make([]byte, 32*nseg*total)
+		var fid [32]byte
+		var got C.uint64_t
+		cfile, cdir := C.CString(file), C.CString(savedir)
+		flags := C.int(C.DM_FP_SEGMENT_FILES)
+		if !writeSegments {
+			flags = 0
+		}
+		runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+		rc := C.dm_full_processing(rs, cfile, cdir, C.uint64_t(chain.SegmentSize), flags,
+			(*C.uint8_t)(unsafe.Pointer(&segd[0])), (*C.uint8_t)(unsafe.Pointer(&fragd[0])), C.uint64_t(nseg), &got,
+			(*C.uint8_t)(unsafe.Pointer(&fid[0])))
+		var err error
+		if rc != C.DM_OK {
+			if msg := C.GoString(C.dm_last_error(nil)); msg != "" {
+				err = errors.New(msg)
+			} else {
+				err = errors.New(C.GoString(C.dm_strerror(rc)))
+			}
+		}
+		runtime.UnlockOSThread()
+		C.free(unsafe.Pointer(cfile))
+		C.free(unsafe.Pointer(cdir))
+		if rc == C.DM_ERR_INVALID && uint64(got) > nseg && attempt == 0 { // the file grew since Stat
+			nseg = uint64(got)
+			continue
+		}
+		if err != nil {
+			return nil, "", err
+		}
+		info := make([]chain.SegmentDataInfo, 0, nseg)
+		for s := uint64(0); s < uint64(got); s++ {
+			names := make([]string, total)
+			for j := uint64(0); j < total; j++ {
+				t := s*total + j
+				names[j] = filepath.Join(savedir, hex.EncodeToString(fragd[32*t:32*t+32]))
+			}
+			info = append(info, chain.SegmentDataInfo{
+				SegmentHash:  filepath.Join(savedir, hex.EncodeToString(segd[32*s:32*s+32])),
+				FragmentHash: names,
+			})
+		}
+		return info, hex.EncodeToString(fid[:]), nil
+	}
 }

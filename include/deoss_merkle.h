@@ -213,6 +213,20 @@ int dm_process_buffer(dm_rs *rs, const void *host, uint64_t len, uint64_t segmen
  * pointers, the arrays or their entries nullable); fids: nobj x 32 bytes. */
 int dm_process_batch(dm_rs *rs, const void *const *objs, const uint64_t *lens, uint64_t nobj, uint64_t segment,
                      void *const *frags_out, uint8_t *const *seg_hashes, uint8_t *const *frag_hashes, uint8_t *fids);
+/* The whole of FullProcessing(file, "", savedir) in one call, from the file path (synchronous):
+ * the file is pread into pinned slots and copied to HBM while its data fragments are written out;
+ * one RS launch and one leaf launch per window of segments (32 GiB of file per window); the
+ * parity fragments come back and are written while the leaf kernel runs; every file is written
+ * under a temporary name in savedir and renamed to savedir/<hex SHA-256> once its digest exists.
+ * With DM_FP_SEGMENT_FILES the zero-padded segments are written too (savedir/<hex segment digest>,
+ * = its data fragments in order).  Outputs: seg_hashes nseg x 32 and frag_hashes nseg x (data +
+ * parity) x 32 (data fragments first; both nullable), fid.  cap = capacity of those arrays in
+ * segments; *nseg_out (nullable) = the file's segment count, also set when cap is too small
+ * (DM_ERR_INVALID).  Errors keep Go's messages ("open <path>: no such file or directory"); an
+ * empty file is DM_ERR_EMPTY "Empty data"; on failure no temporary file is left behind. */
+#define DM_FP_SEGMENT_FILES 1
+int dm_full_processing(dm_rs *rs, const char *path, const char *savedir, uint64_t segment, int flags,
+                       uint8_t *seg_hashes, uint8_t *frag_hashes, uint64_t cap, uint64_t *nseg_out, uint8_t fid[32]);
 
 /* ---- Merkle tree levels and proofs ----------------------------------------
  * cbergoon/merkletree v0.2.0 (go.mod:10) keeps every node of the tree NewHashTree returns

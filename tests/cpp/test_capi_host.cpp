@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <fstream>
+#include <iterator>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -352,6 +353,43 @@ int main(int argc, char** argv) {
             (void)hipFree(dobj);
             (void)hipFree(dpar);
             (void)hipFree(dh);
+            // file form (dm_full_processing): digests, fid and every fragment / segment file;
+            // small slots and windows (test hooks) so slot reuse and the multi-window fid run too
+            const std::string src = tmpdir + "/fp_obj_" + std::to_string(len);
+            const std::string out = tmpdir + "/fp_out_" + std::to_string(len);
+            std::ofstream(src, std::ios::binary).write(reinterpret_cast<const char*>(obj.data()), (std::streamsize)len);
+            for (int hooks = 0; hooks < 2; hooks++) {
+                if (hooks) {
+                    setenv("DEOSS_FP_SLOT_BYTES", "8192", 1);
+                    setenv("DEOSS_FP_WINDOW_BYTES", "8192", 1);
+                }
+                std::vector<uint8_t> fs_(ws.size()), ff(wf.size());
+                uint8_t ffid[32];
+                uint64_t ns = 0;
+                EXPECT(dm_full_processing(rs, src.c_str(), out.c_str(), seg, DM_FP_SEGMENT_FILES, fs_.data(), ff.data(),
+                                          nseg, &ns, ffid) == DM_OK);
+                EXPECT(ns == nseg && fs_ == ws && ff == wf && std::memcmp(ffid, wfid, 32) == 0);
+                static const char* hx = "0123456789abcdef";
+                for (uint64_t t = 0; t < nseg * 12; t++) {
+                    std::string name;
+                    for (int i = 0; i < 32; i++) {
+                        name += hx[wf[32 * t + i] >> 4];
+                        name += hx[wf[32 * t + i] & 15];
+                    }
+                    std::ifstream in(out + "/" + name, std::ios::binary);
+                    std::vector<uint8_t> got((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+                    EXPECT(got.size() == frag && std::memcmp(got.data(), wfr.data() + t * frag, frag) == 0);
+                }
+                unsetenv("DEOSS_FP_SLOT_BYTES");
+                unsetenv("DEOSS_FP_WINDOW_BYTES");
+            }
+            uint64_t ns = 0;
+            EXPECT(dm_full_processing(rs, src.c_str(), out.c_str(), seg, 0, gs.data(), gf.data(), nseg - 1, &ns, gfid) ==
+                       DM_ERR_INVALID && ns == nseg);   // digest arrays one segment short
+            EXPECT(dm_full_processing(rs, (tmpdir + "/fp_missing").c_str(), out.c_str(), seg, 0, nullptr, nullptr, 0,
+                                      nullptr, gfid) == DM_ERR_IO);
+            EXPECT(std::string(dm_last_error(c)) == "open " + tmpdir + "/fp_missing: no such file or directory");
+            std::remove(src.c_str());
         }
         uint8_t fid[32];
         EXPECT(dm_process_buffer(rs, nullptr, 0, seg, nullptr, nullptr, nullptr, fid) == DM_ERR_EMPTY);

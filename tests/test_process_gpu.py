@@ -99,18 +99,27 @@ def test_process_errors(ctx):
     q.close()
 
 
-def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch):
-    """FullProcessing(file, "", savedir): fragment files named by their SHA-256, fid = oracle fid;
-    several GPU windows (the fid then comes from dm_tree_levels over all segment digests)."""
+@pytest.mark.parametrize("path,slot,window", [("windows", None, None), ("one_call", None, None),
+                                              ("one_call", 8192, 3 * 4096), ("one_call", 3 * 4096, 4 * 4096)])
+def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch, path, slot, window):
+    """FullProcessing(file, "", savedir): fragment (and segment) files named by their SHA-256 with
+    the right bytes, fid = oracle fid.  "windows": the window path (several dm_process_buffer
+    calls; the fid then comes from the tree over all segment digests).  "one_call":
+    dm_full_processing, also with small pinned slots (slot reuse, parity sets split over slots)
+    and small windows (several GPU passes, fid over all segments); no temporary file survives."""
     import deoss_amd.process as proc
     from oracle import splitmix64_bytes
     monkeypatch.setattr(proc, "WINDOW_SEGMENTS", 3)
+    if slot:
+        monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", str(slot))
+        monkeypatch.setenv("DEOSS_FP_WINDOW_BYTES", str(window))
     p = _processor(ctx, 4, 8, 4096)
+    run = p.FullProcessingWindows if path == "windows" else p.FullProcessing
     data = splitmix64_bytes(10 * 4096 + 999, 0xDE0552100)
     f = tmp_path / "object.bin"
     f.write_bytes(data)
-    savedir = tmp_path / "cache"
-    info, fid, err = p.FullProcessing(str(f), "", str(savedir))
+    savedir = tmp_path / "cache" / "deeper"
+    info, fid, err = run(str(f), "", str(savedir))
     assert err is None
     seg_b, frag_b, want_fid, frags = oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
     assert fid == want_fid.hex()
@@ -120,16 +129,44 @@ def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch):
         padded = data[s * 4096:(s + 1) * 4096]
         assert open(si.SegmentHash, "rb").read() == padded + bytes(4096 - len(padded))
         assert len(si.FragmentHash) == 12
-        for j, path in enumerate(si.FragmentHash):
+        for j, fp in enumerate(si.FragmentHash):
             t = s * 12 + j
-            assert os.path.basename(path) == frag_b[32 * t:32 * t + 32].hex()
-            assert open(path, "rb").read() == frags[t * 1024:(t + 1) * 1024]
+            assert os.path.basename(fp) == frag_b[32 * t:32 * t + 32].hex()
+            assert open(fp, "rb").read() == frags[t * 1024:(t + 1) * 1024]
+    assert not [n for n in os.listdir(savedir) if n.startswith(".")]
     # errors keep the Go shape: (nil, "", err)
-    assert p.FullProcessing(str(f), "key", str(savedir))[2] is not None
+    assert run(str(f), "key", str(savedir))[2] is not None
     empty = tmp_path / "empty.bin"
     empty.write_bytes(b"")
-    assert str(p.FullProcessing(str(empty), "", str(savedir))[2]) == "Empty data"
-    assert p.FullProcessing(str(tmp_path / "missing"), "", str(savedir))[2] is not None
+    assert str(run(str(empty), "", str(savedir))[2]) == "Empty data"
+    missing = run(str(tmp_path / "missing"), "", str(savedir))[2]
+    assert missing is not None
+    if path == "one_call":
+        assert str(missing) == f"open {tmp_path / 'missing'}: no such file or directory"
+        blocker = tmp_path / "not_a_dir"
+        blocker.write_bytes(b"x")
+        assert run(str(f), "", str(blocker / "sub"))[2] is not None   # savedir under a regular file
+    p.close()
+
+
+@pytest.mark.parametrize("nbytes", [1, 9 * (32 << 20) + 12345])
+def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, nbytes):
+    """dm_full_processing at chain.SegmentSize (32 MiB segments, 4 + 8 fragments of 8 MiB): digests
+    and fid = the oracle's, every file on disk hashes to its name."""
+    from oracle import splitmix64_bytes
+    p = _processor(ctx)
+    data = splitmix64_bytes(nbytes, 0xDE0552200 + nbytes)
+    f = tmp_path / "object.bin"
+    f.write_bytes(data)
+    savedir = tmp_path / "cache"
+    segd, fragd, fid = p.full_processing_file(str(f), str(savedir))
+    want_seg, want_frag, want_fid, _ = oracle_lib.full_processing(data, 32 << 20, 4, 8, nthreads=8)
+    assert (segd, fragd, fid) == (want_seg, want_frag, want_fid)
+    names = sorted(os.listdir(savedir))
+    assert names == sorted({fragd[32 * t:32 * t + 32].hex() for t in range(len(fragd) // 32)} |
+                           {segd[32 * s:32 * s + 32].hex() for s in range(len(segd) // 32)})
+    for n in names[:6]:
+        assert hashlib.sha256(open(savedir / n, "rb").read()).hexdigest() == n
     p.close()
 
 
