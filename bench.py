@@ -93,7 +93,7 @@ def main() -> None:
                          "(other_configs), the e2e host-buffer rates and the 64 KiB / 1 MiB sweep points")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
     ap.add_argument("--workload", default="object",
-                    choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files", "fullprocessing",
+                    choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files", "fullprocessing", "process_upload",
                              "plumbing"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
@@ -144,7 +144,8 @@ def main() -> None:
 
     runners = {"upload": run_upload, "files": run_files, "plumbing": run_plumbing, "rs": run_rs,
                "process": run_process, "proofs": run_proofs, "concurrent": run_concurrent,
-               "batch": run_batch, "stream": run_batch, "fullprocessing": run_fullprocessing}
+               "batch": run_batch, "stream": run_batch, "fullprocessing": run_fullprocessing,
+               "process_upload": run_process_upload}
     if args.workload in runners:
         res = runners[args.workload](args, torch, dist, world, rank, device, dev_index, gloo)
         if res is not None and rank == 0:
@@ -1054,6 +1055,138 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
                                    "kind": "port", "sample": f"{sample_n} segments of the same file through "
                                    "oracle/process_oracle.c (SHA-256 + RS, serial like the SDK; no file writes)"}
         return out
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
+    """§8f #1 + #2: the upload handler's whole flow, body -> file + FullProcessing.  The body
+    (--object-gib, synthetic, in host memory) arrives in --piece-kib pieces; the handler writes each
+    piece to its file (saveObjectToFile, node/objectHandler.go:248-266) and:
+      streamed: hands the same piece to a dm_pstream, and closes it after the last piece (coding,
+        hashing and fragment writes happen while the body arrives);
+      after:    runs dm_full_processing over the saved file (node/objectHandler.go:168 order).
+    One step = the whole flow for one body, files in /dev/shm, savedir emptied (untimed) before
+    each run.  Reported: body GiB/s from the first piece to the fid, and the tail after the last
+    piece."""
+    import shutil
+    import tempfile
+    from deoss_amd import MerkleContext
+    from deoss_amd.process import Processor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    seg, k, m = 32 << 20, 4, 8
+    length = int(args.object_gib * (1 << 30))
+    piece = args.piece_kib << 10
+    nseg = -(-length // seg)
+    orc = Oracle()
+    need = 2 * length + nseg * (k + m + 4) * (seg // k) + (1 << 30)
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > need else None
+    d = tempfile.mkdtemp(prefix="deoss_pu_", dir=base)
+    try:
+        body = torch.empty(length, dtype=torch.uint8)
+        orc.fill_splitmix_ptr(body.data_ptr(), 0, length // 8 * 8, SEED + 0x400)
+        mv = memoryview(body.numpy())
+        addr = body.data_ptr()
+        ctx = MerkleContext(devices=[dev_index])
+        proc = Processor(ctx, k, m, seg)
+        fpath, savedir = os.path.join(d, "upload.bin"), os.path.join(d, "cache")
+
+        def fresh():
+            shutil.rmtree(savedir, ignore_errors=True)
+            if os.path.exists(fpath):
+                os.unlink(fpath)
+
+        def pace(t0, off, rate):   # the body arrives at `rate` B/s (None: as fast as the host goes)
+            if rate:
+                dt = t0 + off / rate - time.perf_counter()
+                if dt > 0:
+                    time.sleep(dt)
+
+        def streamed(nbytes=length, rate=None):
+            t0 = time.perf_counter()
+            st = proc.NewProcessingStream(savedir)
+            with open(fpath, "wb") as f:
+                for off in range(0, nbytes, piece):
+                    pace(t0, off, rate)
+                    n = min(piece, nbytes - off)
+                    f.write(mv[off:off + n])
+                    st.write((addr + off, n))
+            t_last = time.perf_counter()
+            info, fid = st.close()
+            t1 = time.perf_counter()
+            return t1 - t0, t1 - t_last, fid, st
+
+        def after(nbytes=length, rate=None):
+            t0 = time.perf_counter()
+            with open(fpath, "wb") as f:
+                for off in range(0, nbytes, piece):
+                    pace(t0, off, rate)
+                    f.write(mv[off:off + min(piece, nbytes - off)])
+            t_last = time.perf_counter()
+            segd, fragd, fid = proc.full_processing_file(fpath, savedir)
+            t1 = time.perf_counter()
+            return t1 - t0, t1 - t_last, fid.hex(), (segd, fragd)
+
+        res = {}
+        for name, fn in (("streamed", streamed), ("after", after)):
+            for _ in range(args.warmup):
+                fresh()
+                fn()
+            runs = []
+            for _ in range(args.steps):
+                fresh()
+                runs.append(fn())
+            res[name] = runs
+        # the same flows with the body arriving at a network link's rate (2 GiB at 1.25 GB/s = 10 GbE)
+        link, link_bytes = 1.25e9, min(length, 2 << 30)
+        for name, fn in (("streamed_10GbE", streamed), ("after_10GbE", after)):
+            runs = []
+            for _ in range(max(1, args.steps)):
+                fresh()
+                runs.append(fn(link_bytes, link))
+            res[name] = runs
+        s_fid, a_fid = res["streamed"][-1][2], res["after"][-1][2]
+        st = res["streamed"][-1][3]
+        segd, fragd = res["after"][-1][3]
+        # parity: streamed = file form (every digest, the fid); segment digests + fid vs the CPU
+        threads = min(16, os.cpu_count() or 1)
+        host = body.numpy()
+        padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
+        want_seg = orc.root_buffer_ptr(addr, (nseg - 1) * seg, seg, threads, True)[0] if nseg > 1 else b""
+        want_seg = (want_seg or b"") + orc.sha256(padded)
+        want_fid = orc.reduce(want_seg)[:32].hex()
+        parity = {"fid": s_fid, "cpu_fid": want_fid, "segment_digests": nseg,
+                  "bit_exact": bool(s_fid == a_fid == want_fid and st.segment_digests == segd == want_seg
+                                    and st.fragment_digests == fragd)}
+        fresh()
+
+        def summ(runs):
+            tot = sum(r[0] for r in runs) / len(runs)
+            return {"GiBps": round(length / tot / (1 << 30), 4), "ms": round(tot * 1e3, 1),
+                    "tail_ms_after_last_piece": round(sum(r[1] for r in runs) / len(runs) * 1e3, 1),
+                    "step_ms": [round(r[0] * 1e3, 1) for r in runs]}
+
+        sv, av = summ(res["streamed"]), summ(res["after"])
+
+        def summ_link(runs):
+            tot = sum(r[0] for r in runs) / len(runs)
+            return {"GiBps": round(link_bytes / tot / (1 << 30), 4), "ms": round(tot * 1e3, 1),
+                    "tail_ms_after_last_piece": round(sum(r[1] for r in runs) / len(runs) * 1e3, 1)}
+        return {
+            "metric": "GiB/s of upload body through the handler flow: body -> file + FullProcessing (fid, fragment files)",
+            "value": sv["GiBps"], "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": sv["ms"], "higher_is_better": True, "scaling": "none", "vs_baseline": None,
+            "dtype": "u32 (SHA-256), u8 (GF(2^8))",
+            "data": f"synthetic splitmix64 body in host memory, {piece} B pieces, files in "
+                    f"{'/dev/shm' if base else 'the temp dir'}",
+            "config": {"workload": f"1 body of {length} B -> {nseg} segments; the file is written as the pieces arrive",
+                       "object_bytes": length, "piece_bytes": piece},
+            "streamed": sv, "after_file_saved": av,
+            "at_10GbE": {"body_bytes": link_bytes, "link_GBps": link / 1e9,
+                         "streamed": summ_link(res["streamed_10GbE"]), "after_file_saved": summ_link(res["after_10GbE"])},
+            "parity": parity,
+        }
     finally:
         shutil.rmtree(d, ignore_errors=True)
 

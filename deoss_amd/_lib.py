@@ -37,6 +37,7 @@ EXPORTS = (
     "dm_rs_create", "dm_rs_destroy", "dm_rs_matrix", "dm_rs_encode", "dm_rs_encode_buffer", "dm_rs_reconstruct",
     "dm_rs_verify", "dm_rs_encode_device_async", "dm_rs_reconstruct_device_async",
     "dm_process_device_async", "dm_process_buffer", "dm_process_batch", "dm_full_processing",
+    "dm_pstream_open", "dm_pstream_write", "dm_pstream_close", "dm_pstream_abort",
     "dm_tree_node_count", "dm_tree_depth", "dm_tree_levels_device_async", "dm_tree_levels",
     "dm_merkle_paths_device_async", "dm_merkle_paths", "dm_verify_paths_device_async", "dm_verify_paths",
     "dm_verify_object_device_async",
@@ -101,6 +102,10 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_process_buffer": ([vp, vp, u64, u64, vp, vp, vp, vp], i32),
         "dm_process_batch": ([vp, pvp, pu64, u64, u64, pvp, pvp, pvp, vp], i32),
         "dm_full_processing": ([vp, ctypes.c_char_p, ctypes.c_char_p, u64, i32, vp, vp, u64, pu64, vp], i32),
+        "dm_pstream_open": ([vp, u64, ctypes.c_char_p, i32, ctypes.POINTER(vp)], i32),
+        "dm_pstream_write": ([vp, vp, u64], i32),
+        "dm_pstream_close": ([vp, vp, vp, u64, pu64, vp], i32),
+        "dm_pstream_abort": ([vp], None),
         "dm_tree_node_count": ([u64], u64),
         "dm_tree_depth": ([u64], u32),
         "dm_tree_levels_device_async": ([vp, vp, u64, vp, vp], i32),

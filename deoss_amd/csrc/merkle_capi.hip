@@ -1200,5 +1200,6 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
 #include "rs_capi.inl"
 #include "process_capi.inl"
 #include "fullproc_capi.inl"
+#include "process_stream.inl"
 #include "tree_capi.inl"
 #include "batcher.inl"

@@ -1,0 +1,463 @@
+// process_stream.inl -- dm_pstream_*: FullProcessing while the upload body arrives (SURVEY.md 8f
+// #1 + #2).  The upload handlers write the body to a file (node/objectHandler.go:248-266
+// saveObjectToFile, node/fileHandler.go:899-937) and only then run cess-go-sdk
+// FullProcessing(fpath, cipher, cacheDir) over it (node/objectHandler.go:168,
+// node/fileHandler.go:771), which reads the file again.  A pstream takes the body in pieces of any
+// size (io.MultiWriter beside the file) and does the FullProcessing work as the bytes arrive:
+//   - pieces fill a pinned slot of whole segments; a full slot is copied to its own device chunk
+//     (segments + room for their parity), its data fragments and segment files are written to
+//     temporary names by background writers, and one RS launch codes the chunk;
+//   - a chunk's parity comes back through a free slot and is written as soon as its RS launch
+//     (on its own stream, in chunk order) has finished (checked whenever a slot is taken);
+//   - every kPsBatchChunks chunks, one table-mode leaf launch hashes their segments and fragments
+//     on one of two compute streams (the 32 MiB segment chains of one batch run while later
+//     batches arrive);
+//   - close pads the last segment, launches the last chunk and batch, drains the parity, builds
+//     the fid over all segment digests and renames every temporary to savedir/<hex SHA-256>.
+// Results are those of dm_full_processing on the same bytes.  Part of merkle_capi.hip (after
+// fullproc_capi.inl: SlotWrites, write_whole, mkdir_all, hex32, env_bytes).
+
+namespace {
+
+constexpr int kPsSlots = 4;
+constexpr uint64_t kPsSlotBytes = 64ull << 20;
+constexpr uint64_t kPsBatchChunks = 32;   // 64 segments = 2 GiB of body per leaf launch (32 MiB segments)
+
+struct PsChunk {
+    uint64_t s0 = 0, ns = 0;      // segments [s0, s0 + ns)
+    DevBuf mem;                   // ns * seg of data, then ns * pbytes of parity
+    hipEvent_t ev_rs = nullptr;   // RS done: parity may be copied out
+    bool drained = false;
+};
+
+struct PsBatch {
+    uint64_t c0 = 0, nc = 0, s0 = 0, ns = 0;   // chunks [c0, c0 + nc) = segments [s0, s0 + ns)
+    DevBuf tab, dig;                            // leaf table; digests: ns segments, then ns x total fragments
+    PinnedBuf htab;
+    int lane = 0;
+};
+
+}  // namespace
+
+struct dm_pstream {
+    dm_rs* r = nullptr;
+    int k = 0, m = 0, total = 0, flags = 0;
+    uint64_t seg = 0, frag = 0, pbytes = 0, spd = 1, spp = 1, slot_len = 0, batch_chunks = kPsBatchChunks;
+    std::string dir, base;
+    PinnedBuf slot[kPsSlots];
+    hipEvent_t ev_slot[kPsSlots] = {};
+    SlotWrites wr[kPsSlots];
+    bool busy[kPsSlots] = {};
+    uint64_t next_slot = 0;
+    int cur = -1;              // slot being filled, -1: none
+    uint64_t fill = 0;
+    uint64_t received = 0;
+    hipStream_t copy = nullptr, code = nullptr, comp[2] = {nullptr, nullptr};   // H2D/D2H, RS, leaf lanes
+    hipEvent_t ev_copy = nullptr, ev_code = nullptr;
+    std::vector<PsChunk*> chunks;
+    std::vector<PsBatch*> batches;
+    uint64_t hashed_chunks = 0;     // chunks covered by leaf launches
+    uint64_t drained_upto = 0;      // chunks [0, drained_upto) have their parity written
+    std::vector<std::pair<std::string, uint64_t>> pend;   // temporary, digest index (~: segment)
+    std::string err;
+};
+
+namespace {
+
+int pfail(dm_pstream* st, int code, const std::string& msg) {
+    st->err = msg;
+    t_err = msg;
+    return code;
+}
+
+#define PSHIP(expr)                                                                              \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return pfail(st, e_ == hipErrorOutOfMemory ? DM_ERR_NOMEM : DM_ERR_HIP,               \
+                         std::string(#expr) + ": " + hipGetErrorString(e_));                     \
+    } while (0)
+
+Dev& ps_dev(dm_pstream* st) { return st->r->c->devs[0]; }
+
+// A free slot (its H2D / D2H finished and its writes joined).
+int ps_take_slot(dm_pstream* st, int* out) {
+    const int sl = (int)(st->next_slot++ % kPsSlots);
+    if (st->busy[sl]) {
+        PSHIP(hipEventSynchronize(st->ev_slot[sl]));
+        const std::string e = st->wr[sl].wait();
+        if (!e.empty()) return pfail(st, DM_ERR_IO, e);
+        st->busy[sl] = false;
+    }
+    *out = sl;
+    return DM_OK;
+}
+
+// Copy chunk ci's parity out through a slot and write its parity fragments (RS must be done).
+int ps_drain_chunk(dm_pstream* st, uint64_t ci) {
+    PsChunk* ch = st->chunks[ci];
+    uint8_t* parity = ch->mem.u8() + ch->ns * st->seg;
+    for (uint64_t t0 = 0; t0 < ch->ns; t0 += st->spp) {
+        const uint64_t nt = std::min(st->spp, ch->ns - t0);
+        int sl;
+        int rc = ps_take_slot(st, &sl);
+        if (rc != DM_OK) return rc;
+        uint8_t* buf = st->slot[sl].u8();
+        PSHIP(hipStreamWaitEvent(st->copy, ch->ev_rs, 0));
+        PSHIP(hipMemcpyAsync(buf, parity + t0 * st->pbytes, nt * st->pbytes, hipMemcpyDeviceToHost, st->copy));
+        PSHIP(hipEventRecord(st->ev_slot[sl], st->copy));
+        PSHIP(hipEventSynchronize(st->ev_slot[sl]));
+        std::vector<FpFile> files;
+        for (uint64_t u = 0; u < nt; u++) {
+            const uint64_t gs = ch->s0 + t0 + u;
+            for (int i = 0; i < st->m; i++) {
+                const uint64_t id = gs * (uint64_t)st->total + (uint64_t)(st->k + i);
+                files.push_back({buf + u * st->pbytes + (uint64_t)i * st->frag, st->frag,
+                                 st->base + "f" + std::to_string(id)});
+                st->pend.emplace_back(files.back().tmp, 32 * id);
+            }
+        }
+        st->wr[sl].start(std::move(files));
+        st->busy[sl] = true;
+    }
+    ch->drained = true;
+    return DM_OK;
+}
+
+// Drain every chunk, in order, whose RS launch has finished (all of them when `all`).
+int ps_drain(dm_pstream* st, bool all) {
+    while (st->drained_upto < st->chunks.size()) {
+        PsChunk* ch = st->chunks[st->drained_upto];
+        if (!all) {
+            const hipError_t q = hipEventQuery(ch->ev_rs);
+            if (q == hipErrorNotReady) break;
+            PSHIP(q);
+        }
+        int rc = ps_drain_chunk(st, st->drained_upto);
+        if (rc != DM_OK) return rc;
+        st->drained_upto++;
+    }
+    return DM_OK;
+}
+
+// One table-mode leaf launch over chunks [hashed_chunks, upto): segments first, then fragments.
+int ps_launch_batch(dm_pstream* st, uint64_t upto) {
+    if (upto <= st->hashed_chunks) return DM_OK;
+    Dev& d = ps_dev(st);
+    PsBatch* b = new PsBatch();
+    st->batches.push_back(b);
+    b->c0 = st->hashed_chunks;
+    b->nc = upto - b->c0;
+    b->s0 = st->chunks[b->c0]->s0;
+    for (uint64_t c = b->c0; c < upto; c++) b->ns += st->chunks[c]->ns;
+    const uint64_t T = b->ns * (1 + (uint64_t)st->total);
+    PSHIP(b->htab.ensure(16 * T));
+    PSHIP(b->tab.ensure(16 * T));
+    PSHIP(b->dig.ensure(32 * T));
+    uint64_t* addr = reinterpret_cast<uint64_t*>(b->htab.p);
+    uint64_t* lens = addr + T;
+    uint64_t i = 0;
+    for (uint64_t c = b->c0; c < upto; c++) {
+        PsChunk* ch = st->chunks[c];
+        for (uint64_t u = 0; u < ch->ns; u++, i++) {
+            addr[i] = reinterpret_cast<uint64_t>(ch->mem.u8() + u * st->seg);
+            lens[i] = st->seg;
+        }
+    }
+    for (uint64_t c = b->c0; c < upto; c++) {
+        PsChunk* ch = st->chunks[c];
+        const uint8_t* parity = ch->mem.u8() + ch->ns * st->seg;
+        for (uint64_t u = 0; u < ch->ns; u++)
+            for (int j = 0; j < st->total; j++, i++) {
+                addr[i] = reinterpret_cast<uint64_t>(
+                    j < st->k ? ch->mem.u8() + u * st->seg + (uint64_t)j * st->frag
+                              : parity + (u * st->m + (uint64_t)(j - st->k)) * st->frag);
+                lens[i] = st->frag;
+            }
+    }
+    b->lane = (int)(st->batches.size() % 2);
+    hipStream_t s = st->comp[b->lane];
+    // after the RS launches of these chunks (in order on the code stream); batches on the two
+    // lanes overlap, so one batch's segment chains run while the next batch arrives
+    PSHIP(hipEventRecord(st->ev_code, st->code));
+    PSHIP(hipStreamWaitEvent(s, st->ev_code, 0));
+    PSHIP(hipMemcpyAsync(b->tab.p, b->htab.p, 16 * T, hipMemcpyHostToDevice, s));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(b->tab.p);
+    la.lens = la.addrs + T;
+    la.nleaves = T;
+    la.byte_end = ~0ull;
+    la.digests = b->dig.u8();
+    launch_leaves_t<true, true>(s, la, pick_leaf_kernel(st->r->c, d, T), d.cus);
+    PSHIP(hipGetLastError());
+    st->hashed_chunks = upto;
+    return DM_OK;
+}
+
+// The current slot holds `len` bytes (whole segments, the last one zero-padded at close): copy it
+// to a new device chunk, write its data fragments and segments, code it.
+int ps_flush(dm_pstream* st) {
+    if (st->cur < 0 || st->fill == 0) return DM_OK;
+    Dev& d = ps_dev(st);
+    const int sl = st->cur;
+    const uint64_t ns = ceil_div(st->fill, st->seg), len = ns * st->seg;
+    uint8_t* buf = st->slot[sl].u8();
+    if (len > st->fill) std::memset(buf + st->fill, 0, len - st->fill);
+    PsChunk* ch = new PsChunk();
+    st->chunks.push_back(ch);
+    ch->s0 = st->chunks.size() > 1 ? st->chunks[st->chunks.size() - 2]->s0 + st->chunks[st->chunks.size() - 2]->ns : 0;
+    ch->ns = ns;
+    PSHIP(hipEventCreateWithFlags(&ch->ev_rs, hipEventDisableTiming));
+    PSHIP(ch->mem.ensure(ns * (st->seg + st->pbytes)));
+    PSHIP(hipMemcpyAsync(ch->mem.p, buf, len, hipMemcpyHostToDevice, st->copy));
+    PSHIP(hipEventRecord(st->ev_slot[sl], st->copy));
+    std::vector<FpFile> files;
+    for (uint64_t u = 0; u < ns; u++) {
+        const uint64_t gs = ch->s0 + u;
+        for (int j = 0; j < st->k; j++) {
+            const uint64_t id = gs * (uint64_t)st->total + (uint64_t)j;
+            files.push_back({buf + u * st->seg + (uint64_t)j * st->frag, st->frag, st->base + "f" + std::to_string(id)});
+            st->pend.emplace_back(files.back().tmp, 32 * id);
+        }
+        if (st->flags & DM_FP_SEGMENT_FILES) {
+            files.push_back({buf + u * st->seg, st->seg, st->base + "s" + std::to_string(gs)});
+            st->pend.emplace_back(files.back().tmp, ~(32 * gs));
+        }
+    }
+    st->wr[sl].start(std::move(files));
+    st->busy[sl] = true;
+    st->cur = -1;
+    st->fill = 0;
+    // RS on the code stream after the H2D
+    hipStream_t s = st->code;
+    PSHIP(hipEventRecord(st->ev_copy, st->copy));
+    PSHIP(hipStreamWaitEvent(s, st->ev_copy, 0));
+    dm::RsArgs a{};
+    for (int j = 0; j < st->k; j++) a.in[j] = ch->mem.u8() + (uint64_t)j * st->frag;
+    uint8_t* parity = ch->mem.u8() + len;
+    for (int i = 0; i < st->m; i++) a.out[i] = parity + (uint64_t)i * st->frag;
+    a.in_seg_stride = st->seg;
+    a.out_seg_stride = st->pbytes;
+    a.units_per_seg = st->frag / 16;
+    a.nseg = ns;
+    a.table = static_cast<const uint2*>(st->r->enc_tab.p);
+    a.nout = (uint32_t)st->m;
+    launch_rs(d, s, st->k, a);
+    PSHIP(hipGetLastError());
+    PSHIP(hipEventRecord(ch->ev_rs, s));
+    if (st->chunks.size() - st->hashed_chunks >= st->batch_chunks) return ps_launch_batch(st, st->chunks.size());
+    return DM_OK;
+}
+
+void ps_free(dm_pstream* st) {
+    if (!st) return;
+    (void)hipSetDevice(ps_dev(st).id);
+    for (hipStream_t s : {st->copy, st->code, st->comp[0], st->comp[1]})
+        if (s) (void)hipStreamSynchronize(s);
+    for (auto& w : st->wr) (void)w.wait();
+    for (PsChunk* ch : st->chunks) {
+        ch->mem.release();
+        if (ch->ev_rs) (void)hipEventDestroy(ch->ev_rs);
+        delete ch;
+    }
+    for (PsBatch* b : st->batches) {
+        b->tab.release();
+        b->dig.release();
+        b->htab.release();
+        delete b;
+    }
+    for (auto& b : st->slot) b.release();
+    for (hipEvent_t e : st->ev_slot)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {st->ev_copy, st->ev_code})
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t s : {st->copy, st->code, st->comp[0], st->comp[1]})
+        if (s) (void)hipStreamDestroy(s);
+    delete st;
+}
+
+void ps_unlink_pending(dm_pstream* st) {
+    for (const auto& p : st->pend)
+        if (!p.first.empty()) ::unlink(p.first.c_str());
+}
+
+}  // namespace
+
+extern "C" {
+
+int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, dm_pstream** out) {
+    if (!r || !savedir || !out) return bad_arg();
+    *out = nullptr;
+    dm_ctx* c = r->c;
+    {
+        CallLock lk(c->mu);
+        RC_TRY(process_check(r, 1, segment));
+    }
+    DeviceRestore dev;
+    dm_pstream* st = new dm_pstream();
+    st->r = r;
+    st->k = r->k;
+    st->m = r->m;
+    st->total = r->k + r->m;
+    st->flags = flags;
+    st->seg = segment;
+    st->frag = segment / (uint64_t)r->k;
+    st->pbytes = (uint64_t)r->m * st->frag;
+    // test hooks (env, read at open): small slots / batches exercise slot reuse and many launches
+    const uint64_t slot_bytes = env_bytes("DEOSS_FP_SLOT_BYTES", kPsSlotBytes);
+    st->batch_chunks = env_bytes("DEOSS_PS_BATCH_CHUNKS", kPsBatchChunks);
+    st->spd = std::max<uint64_t>(1, slot_bytes / segment);
+    st->spp = std::max<uint64_t>(1, slot_bytes / st->pbytes);
+    st->slot_len = st->spd * segment;
+    st->dir = savedir;
+    while (st->dir.size() > 1 && st->dir.back() == '/') st->dir.pop_back();
+    st->base = st->dir + "/.dm-ps-" + std::to_string((long long)::getpid()) + "-" +
+               std::to_string((unsigned long long)g_fp_seq++) + "-";
+    int rc = DM_OK;
+    do {
+        const std::string me = mkdir_all(st->dir);
+        if (!me.empty()) { rc = pfail(st, DM_ERR_IO, me); break; }
+        hipError_t e;
+        if ((e = hipSetDevice(ps_dev(st).id)) != hipSuccess) { rc = pfail(st, DM_ERR_HIP, "hipSetDevice"); break; }
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if ((e = hipStreamCreateWithPriority(&st->copy, hipStreamNonBlocking, hi)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&st->code, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&st->comp[0], hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&st->comp[1], hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&st->ev_copy, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&st->ev_code, hipEventDisableTiming)) != hipSuccess) {
+            rc = pfail(st, DM_ERR_HIP, std::string("stream: ") + hipGetErrorString(e));
+            break;
+        }
+        const uint64_t cap = std::max(st->slot_len, st->spp * st->pbytes);
+        for (int i = 0; i < kPsSlots && rc == DM_OK; i++) {
+            if ((e = hipEventCreateWithFlags(&st->ev_slot[i], hipEventDisableTiming)) != hipSuccess ||
+                (e = st->slot[i].ensure(cap)) != hipSuccess)
+                rc = pfail(st, DM_ERR_NOMEM, std::string("pinned slots: ") + hipGetErrorString(e));
+        }
+    } while (0);
+    if (rc != DM_OK) {
+        ps_free(st);
+        return rc;
+    }
+    *out = st;
+    return DM_OK;
+}
+
+int dm_pstream_write(dm_pstream* st, const void* data, uint64_t len) {
+    if (!st || (!data && len)) return bad_arg();
+    DeviceRestore dev;
+    PSHIP(hipSetDevice(ps_dev(st).id));
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    while (len) {
+        if (st->cur < 0) {
+            int rc = ps_drain(st, false);   // parity of coded chunks out first: frees slots early
+            if (rc == DM_OK) rc = ps_take_slot(st, &st->cur);
+            if (rc != DM_OK) return rc;
+        }
+        const uint64_t take = std::min(len, st->slot_len - st->fill);
+        std::memcpy(st->slot[st->cur].u8() + st->fill, p, take);
+        st->fill += take;
+        st->received += take;
+        p += take;
+        len -= take;
+        if (st->fill == st->slot_len) {
+            int rc = ps_flush(st);
+            if (rc != DM_OK) return rc;
+        }
+    }
+    return DM_OK;
+}
+
+int dm_pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out,
+                     uint8_t fid[32]) {
+    if (!st) return bad_arg();
+    DeviceRestore dev;
+    dm_ctx* c = st->r->c;
+    const uint64_t nseg = ceil_div(st->received, st->seg);
+    if (nseg_out) *nseg_out = nseg;
+    int rc = DM_OK;
+    do {
+        if (!fid) { rc = bad_arg(); break; }
+        if (st->received == 0) { rc = pfail(st, DM_ERR_EMPTY, "Empty data"); break; }
+        if ((seg_hashes || frag_hashes) && cap < nseg) {
+            rc = pfail(st, DM_ERR_INVALID, "dm_pstream_close: " + std::to_string(nseg) + " segments, digest arrays hold " +
+                                               std::to_string(cap));
+            break;
+        }
+        if (hipSetDevice(ps_dev(st).id) != hipSuccess) { rc = pfail(st, DM_ERR_HIP, "hipSetDevice"); break; }
+        if ((rc = ps_flush(st)) != DM_OK) break;
+        if ((rc = ps_launch_batch(st, st->chunks.size())) != DM_OK) break;
+        if ((rc = ps_drain(st, true)) != DM_OK) break;
+        // digests: batch b holds its ns segments, then ns x total fragments
+        std::vector<uint8_t> segd(32 * nseg), fragd(32 * nseg * st->total);
+        for (PsBatch* b : st->batches) {
+            hipStream_t s = st->comp[b->lane];
+            hipError_t e;
+            if ((e = hipMemcpyAsync(segd.data() + 32 * b->s0, b->dig.p, 32 * b->ns, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                (e = hipMemcpyAsync(fragd.data() + 32 * b->s0 * st->total, b->dig.u8() + 32 * b->ns,
+                                    32 * b->ns * st->total, hipMemcpyDeviceToHost, s)) != hipSuccess) {
+                rc = pfail(st, DM_ERR_HIP, std::string("digests: ") + hipGetErrorString(e));
+                break;
+            }
+        }
+        if (rc != DM_OK) break;
+        for (hipStream_t s : {st->comp[0], st->comp[1], st->code, st->copy})
+            if (hipStreamSynchronize(s) != hipSuccess) { rc = pfail(st, DM_ERR_HIP, "stream sync"); break; }
+        if (rc != DM_OK) break;
+        for (auto& w : st->wr) {
+            const std::string e = w.wait();
+            if (!e.empty() && rc == DM_OK) rc = pfail(st, DM_ERR_IO, e);
+        }
+        if (rc != DM_OK) break;
+        {   // fid: the tree over every segment digest, on the context
+            CallLock lk(c->mu);
+            Dev& d = ps_dev(st);
+            hipStream_t s = d.stream;
+            if ((rc = begin_call(c, d, s)) != DM_OK) break;
+            hipError_t e;
+            if ((e = d.leaves.ensure(32 * nseg)) != hipSuccess ||
+                (e = hipMemcpyAsync(d.leaves.p, segd.data(), 32 * nseg, hipMemcpyHostToDevice, s)) != hipSuccess) {
+                rc = pfail(st, DM_ERR_HIP, std::string("fid: ") + hipGetErrorString(e));
+                break;
+            }
+            if ((rc = finish(c, d, s, d.leaves.u8(), nseg, true, d.root.u8())) != DM_OK) break;
+            if ((e = hipMemcpyAsync(fid, d.root.p, 32, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                (e = hipStreamSynchronize(s)) != hipSuccess) {
+                rc = pfail(st, DM_ERR_HIP, std::string("fid: ") + hipGetErrorString(e));
+                break;
+            }
+        }
+        for (auto& p : st->pend) {
+            const uint64_t at = p.second;
+            const uint8_t* dig = (at >> 63) ? segd.data() + ~at : fragd.data() + at;
+            const std::string to = st->dir + "/" + hex32(dig);
+            if (::rename(p.first.c_str(), to.c_str()) != 0) {
+                rc = pfail(st, DM_ERR_IO, "rename " + p.first + " " + to + ": " + go_errno(errno));
+                break;
+            }
+            p.first.clear();
+        }
+        if (rc != DM_OK) break;
+        if (seg_hashes) std::memcpy(seg_hashes, segd.data(), segd.size());
+        if (frag_hashes) std::memcpy(frag_hashes, fragd.data(), fragd.size());
+    } while (0);
+    if (rc != DM_OK) {
+        t_err = st->err.empty() ? t_err : st->err;
+        for (auto& w : st->wr) (void)w.wait();
+        ps_unlink_pending(st);
+    }
+    ps_free(st);
+    return rc;
+}
+
+void dm_pstream_abort(dm_pstream* st) {
+    if (!st) return;
+    DeviceRestore dev;
+    for (auto& w : st->wr) (void)w.wait();
+    ps_unlink_pending(st);
+    ps_free(st);
+}
+
+}  // extern "C"

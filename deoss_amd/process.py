@@ -173,6 +173,10 @@ class Processor:
             info.append(SegmentDataInfo(os.path.join(savedir, segd[32 * s:32 * s + 32].hex()), names))
         return info, fid.hex(), None
 
+    def NewProcessingStream(self, savedir: str, segment_files: bool = True) -> "ProcessingStream":
+        """FullProcessing while the body arrives: write() the pieces, close() -> (info, fid)."""
+        return ProcessingStream(self, savedir, segment_files)
+
     def FullProcessingWindows(self, file: str, cipher: str, savedir: str
                               ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
         """The window path (the Go shim's shape before dm_full_processing): read a window of
@@ -220,6 +224,87 @@ class Processor:
         if len(seg_digests) * self.segment > window:   # several windows: tree over all segments
             fid = self.ctx.tree_root(b"".join(seg_digests))
         return info, fid.hex(), None
+
+
+class ProcessingStream:
+    """FullProcessing while the upload body arrives (``dm_pstream_*``): ``write()`` pieces of any
+    size beside the handler's own file write, ``close()`` -> (SegmentDataInfo list, hex fid) with
+    every fragment and segment file in ``savedir`` -- the same results as
+    ``FullProcessing(file, "", savedir)`` on the same bytes, without reading the file again."""
+
+    def __init__(self, proc: "Processor", savedir: str, segment_files: bool = True):
+        self._p = proc
+        self._L = proc.ctx._L
+        self.savedir = savedir
+        self.written = 0
+        h = ctypes.c_void_p()
+        rc = self._L.dm_pstream_open(proc.enc._h, proc.segment, os.fsencode(savedir), 1 if segment_files else 0,
+                                     ctypes.byref(h))
+        self._raise(rc, "dm_pstream_open")
+        self._h = h
+
+    def _raise(self, rc: int, what: str) -> None:
+        if rc == 0:
+            return
+        detail = (self._L.dm_last_error(None) or b"").decode()
+        if rc == DM_ERR_EMPTY:
+            raise DeossMerkleError(rc, "Empty data")
+        if rc == DM_ERR_IO:
+            raise DeossMerkleError(rc, detail)
+        raise DeossMerkleError(rc, f"{what}: {self._L.dm_strerror(rc).decode()}: {detail}")
+
+    def write(self, data) -> int:
+        """One piece: bytes-like, or (address, length) of host memory."""
+        if self._h is None:
+            raise DeossMerkleError(DM_ERR_INVALID, "stream is closed")
+        if isinstance(data, tuple):
+            addr, n = data
+            ptr = ctypes.c_void_p(addr)
+        elif isinstance(data, bytes):
+            n, ptr = len(data), ctypes.c_char_p(data)   # no copy
+        else:
+            mv = memoryview(data).cast("B")
+            n = mv.nbytes
+            ptr = ctypes.c_char_p(mv.tobytes()) if (mv.readonly or n == 0) else (ctypes.c_char * n).from_buffer(mv)
+        rc = self._L.dm_pstream_write(self._h, ptr, n)
+        if rc != 0:
+            self.abort()
+            self._raise(rc, "dm_pstream_write")
+        self.written += n
+        return n
+
+    def close(self) -> Tuple[List[SegmentDataInfo], str]:
+        if self._h is None:
+            raise DeossMerkleError(DM_ERR_INVALID, "stream is closed")
+        p = self._p
+        total = p.k + p.m
+        cap = max(1, (self.written + p.segment - 1) // p.segment)
+        seg = ctypes.create_string_buffer(32 * cap)
+        frag = ctypes.create_string_buffer(32 * cap * total)
+        fid = ctypes.create_string_buffer(32)
+        nseg = ctypes.c_uint64(0)
+        h, self._h = self._h, None
+        self._raise(self._L.dm_pstream_close(h, seg, frag, cap, ctypes.byref(nseg), fid), "dm_pstream_close")
+        n = nseg.value
+        info = []
+        for s in range(n):
+            names = [os.path.join(self.savedir, frag.raw[32 * (s * total + j):32 * (s * total + j + 1)].hex())
+                     for j in range(total)]
+            info.append(SegmentDataInfo(os.path.join(self.savedir, seg.raw[32 * s:32 * s + 32].hex()), names))
+        self.segment_digests = seg.raw[:32 * n]
+        self.fragment_digests = frag.raw[:32 * n * total]
+        return info, fid.raw.hex()
+
+    def abort(self) -> None:
+        if self._h is not None:
+            self._L.dm_pstream_abort(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.abort()
+        except Exception:
+            pass
 
 
 _default: Optional[Processor] = None

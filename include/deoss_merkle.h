@@ -228,6 +228,22 @@ int dm_process_batch(dm_rs *rs, const void *const *objs, const uint64_t *lens, u
 int dm_full_processing(dm_rs *rs, const char *path, const char *savedir, uint64_t segment, int flags,
                        uint8_t *seg_hashes, uint8_t *frag_hashes, uint64_t cap, uint64_t *nseg_out, uint8_t fid[32]);
 
+/* FullProcessing while the upload body arrives (SURVEY.md 8f #1 + #2): the handlers write the body
+ * to a file (node/objectHandler.go:248-266, node/fileHandler.go:899-937) and then run
+ * FullProcessing(fpath, "", cacheDir) over it (node/objectHandler.go:168, node/fileHandler.go:771).
+ * A pstream takes the body in pieces of any size beside that file write: whole segments are
+ * copied to HBM, coded and their fragment files written as they arrive, segments are hashed in
+ * batches on the GPU meanwhile; close pads the last segment, finishes, and returns the same
+ * digests / fid / files as dm_full_processing on the same bytes (flags: DM_FP_SEGMENT_FILES).
+ * Not thread-safe per stream; separate streams (on one rs) may run concurrently.  close and abort
+ * free the stream; on any failure no temporary file is left in savedir. */
+typedef struct dm_pstream dm_pstream;
+int dm_pstream_open(dm_rs *rs, uint64_t segment, const char *savedir, int flags, dm_pstream **out);
+int dm_pstream_write(dm_pstream *st, const void *data, uint64_t len);
+int dm_pstream_close(dm_pstream *st, uint8_t *seg_hashes, uint8_t *frag_hashes, uint64_t cap, uint64_t *nseg_out,
+                     uint8_t fid[32]);
+void dm_pstream_abort(dm_pstream *st);
+
 /* ---- Merkle tree levels and proofs ----------------------------------------
  * cbergoon/merkletree v0.2.0 (go.mod:10) keeps every node of the tree NewHashTree returns
  * (common/hashtree/types.go:38) for GetMerklePath, VerifyContent and VerifyTree.  Here the nodes

@@ -383,6 +383,31 @@ int main(int argc, char** argv) {
                 unsetenv("DEOSS_FP_SLOT_BYTES");
                 unsetenv("DEOSS_FP_WINDOW_BYTES");
             }
+            // streamed form (dm_pstream): random pieces, small slots and batches, then an aborted one
+            for (int hooks = 0; hooks < 2; hooks++) {
+                if (hooks) {
+                    setenv("DEOSS_FP_SLOT_BYTES", "8192", 1);
+                    setenv("DEOSS_PS_BATCH_CHUNKS", "2", 1);
+                }
+                dm_pstream* ps = nullptr;
+                EXPECT(dm_pstream_open(rs, seg, (out + "_ps").c_str(), DM_FP_SEGMENT_FILES, &ps) == DM_OK);
+                std::mt19937_64 rng(len * 7 + hooks);
+                for (uint64_t pos = 0; pos < len;) {
+                    const uint64_t m = std::min<uint64_t>(len - pos, 1 + rng() % 7000);
+                    EXPECT(dm_pstream_write(ps, obj.data() + pos, m) == DM_OK);
+                    pos += m;
+                }
+                std::vector<uint8_t> ps_s(ws.size()), ps_f(wf.size());
+                uint8_t pfid[32];
+                uint64_t pn = 0;
+                EXPECT(dm_pstream_close(ps, ps_s.data(), ps_f.data(), nseg, &pn, pfid) == DM_OK);
+                EXPECT(pn == nseg && ps_s == ws && ps_f == wf && std::memcmp(pfid, wfid, 32) == 0);
+                EXPECT(dm_pstream_open(rs, seg, (out + "_ab").c_str(), 0, &ps) == DM_OK);
+                EXPECT(dm_pstream_write(ps, obj.data(), len) == DM_OK);
+                dm_pstream_abort(ps);
+                unsetenv("DEOSS_FP_SLOT_BYTES");
+                unsetenv("DEOSS_PS_BATCH_CHUNKS");
+            }
             uint64_t ns = 0;
             EXPECT(dm_full_processing(rs, src.c_str(), out.c_str(), seg, 0, gs.data(), gf.data(), nseg - 1, &ns, gfid) ==
                        DM_ERR_INVALID && ns == nseg);   // digest arrays one segment short

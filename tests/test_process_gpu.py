@@ -170,6 +170,89 @@ def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, nbyte
     p.close()
 
 
+def _pieces(data, rng, most):
+    pos = 0
+    while pos < len(data):
+        n = min(len(data) - pos, rng.randint(1, most))
+        yield data[pos:pos + n]
+        pos += n
+
+
+@pytest.mark.parametrize("slot,batch", [(None, None), (8192, 2), (3 * 4096, 1)])
+def test_processing_stream_small(ctx, oracle_lib, tmp_path, monkeypatch, slot, batch):
+    """dm_pstream: the body in random pieces -> the same digests, fid and files as the oracle;
+    small slots / batches (test hooks) make every chunk its own RS launch and batches of 1-2 chunks
+    hash concurrently on the two lanes; no temporary file survives."""
+    from oracle import splitmix64_bytes
+    if slot:
+        monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", str(slot))
+        monkeypatch.setenv("DEOSS_PS_BATCH_CHUNKS", str(batch))
+    p = _processor(ctx, 4, 8, 4096)
+    rng = random.Random(slot or 1)
+    for n in (1, 4096, 4097, 23 * 4096 + 555):
+        data = splitmix64_bytes(n, 0xDE0552300 + n)
+        savedir = tmp_path / f"cache{n}"
+        st = p.NewProcessingStream(str(savedir))
+        for piece in _pieces(data, rng, 9000):
+            st.write(piece)
+        info, fid = st.close()
+        seg_b, frag_b, want_fid, frags = oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
+        assert fid == want_fid.hex()
+        assert st.segment_digests == seg_b and st.fragment_digests == frag_b
+        assert len(info) == -(-n // 4096)
+        for s_i, si in enumerate(info):
+            padded = data[s_i * 4096:(s_i + 1) * 4096]
+            assert open(si.SegmentHash, "rb").read() == padded + bytes(4096 - len(padded))
+            for j, fp in enumerate(si.FragmentHash):
+                t = s_i * 12 + j
+                assert open(fp, "rb").read() == frags[t * 1024:(t + 1) * 1024]
+        assert not [x for x in os.listdir(savedir) if x.startswith(".")]
+    p.close()
+
+
+def test_processing_stream_full_segments_and_errors(ctx, oracle_lib, tmp_path):
+    """32 MiB segments through dm_pstream in 1 B .. 3 MiB pieces = dm_full_processing on the same
+    file = the oracle; two streams at once on one coder; empty and aborted streams leave nothing."""
+    import threading
+    from deoss_amd import DeossMerkleError
+    from oracle import splitmix64_bytes
+    p = _processor(ctx)
+    n = 9 * (32 << 20) + 12345
+    data = splitmix64_bytes(n, 0xDE0552400)
+    want_seg, want_frag, want_fid, _ = oracle_lib.full_processing(data, 32 << 20, 4, 8, nthreads=8)
+    results = {}
+
+    def upload(tag, seed):
+        st = p.NewProcessingStream(str(tmp_path / tag))
+        for piece in _pieces(data, random.Random(seed), 3 << 20):
+            st.write(piece)
+        info, fid = st.close()
+        results[tag] = (st.segment_digests, st.fragment_digests, fid, len(info))
+
+    th = [threading.Thread(target=upload, args=(f"u{i}", i)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for tag in ("u0", "u1"):
+        assert results[tag] == (want_seg, want_frag, want_fid.hex(), 10)
+        names = set(os.listdir(tmp_path / tag))   # equal contents share a name (zero fragments)
+        want_names = {want_frag[i:i + 32].hex() for i in range(0, len(want_frag), 32)} | \
+                     {want_seg[i:i + 32].hex() for i in range(0, len(want_seg), 32)}
+        assert names == want_names
+    f = tmp_path / "obj.bin"
+    f.write_bytes(data)
+    assert p.full_processing_file(str(f), str(tmp_path / "file_form"))[2] == want_fid
+    empty = p.NewProcessingStream(str(tmp_path / "empty"))
+    with pytest.raises(DeossMerkleError, match="Empty data"):
+        empty.close()
+    aborted = p.NewProcessingStream(str(tmp_path / "aborted"))
+    aborted.write(data[:200 << 20])
+    aborted.abort()
+    assert os.listdir(tmp_path / "aborted") == []
+    p.close()
+
+
 # ---- Merkle proofs -----------------------------------------------------------------------------
 
 def test_proof_golden_paths(ctx, pg):
