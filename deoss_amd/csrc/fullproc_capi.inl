@@ -274,6 +274,11 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
     std::vector<uint8_t> segd(32 * nseg), fragd(32 * nseg * total);
     std::vector<std::pair<std::string, uint64_t>> pend;
     int rc = full_processing_windows(r, fs, dir, segment, flags, segd, fragd, pend, fid);
+    if (rc != DM_OK) {   // a failed call may leave copies queued: none may land in a slot the next call fills
+        Dev& d = c->devs[0];
+        (void)hipStreamSynchronize(d.copy);
+        (void)hipStreamSynchronize(d.stream);
+    }
     for (size_t i = 0; rc == DM_OK && i < pend.size(); i++) {
         const uint64_t at = pend[i].second;
         const uint8_t* dig = (at >> 63) ? segd.data() + ~at : fragd.data() + at;

@@ -80,9 +80,11 @@ int pfail(dm_pstream* st, int code, const std::string& msg) {
 
 Dev& ps_dev(dm_pstream* st) { return st->r->c->devs[0]; }
 
-// A free slot (its H2D / D2H finished and its writes joined).
+// A free slot (its H2D / D2H finished and its writes joined).  Slots are pinned on first use, so a
+// small body holds one slot, not four.
 int ps_take_slot(dm_pstream* st, int* out) {
     const int sl = (int)(st->next_slot++ % kPsSlots);
+    if (!st->slot[sl].p) PSHIP(st->slot[sl].ensure(std::max(st->slot_len, st->spp * st->pbytes)));
     if (st->busy[sl]) {
         PSHIP(hipEventSynchronize(st->ev_slot[sl]));
         const std::string e = st->wr[sl].wait();
@@ -330,11 +332,9 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
             rc = pfail(st, DM_ERR_HIP, std::string("stream: ") + hipGetErrorString(e));
             break;
         }
-        const uint64_t cap = std::max(st->slot_len, st->spp * st->pbytes);
         for (int i = 0; i < kPsSlots && rc == DM_OK; i++) {
-            if ((e = hipEventCreateWithFlags(&st->ev_slot[i], hipEventDisableTiming)) != hipSuccess ||
-                (e = st->slot[i].ensure(cap)) != hipSuccess)
-                rc = pfail(st, DM_ERR_NOMEM, std::string("pinned slots: ") + hipGetErrorString(e));
+            if ((e = hipEventCreateWithFlags(&st->ev_slot[i], hipEventDisableTiming)) != hipSuccess)
+                rc = pfail(st, DM_ERR_HIP, std::string("events: ") + hipGetErrorString(e));
         }
     } while (0);
     if (rc != DM_OK) {

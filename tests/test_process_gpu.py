@@ -485,3 +485,19 @@ def test_batcher_process_concurrent(oracle_lib):
     with pytest.raises(DeossMerkleError):
         b.root(b"x")          # wrong mode
     b.close()
+
+
+def test_cpp_process_mirror(tmp_path):
+    """Compile and run tests/cpp/test_process.cpp: the C++ mirror of the Go process shim
+    (include/deoss_process.hpp: FullProcessing over a file, the streaming Writer, Go's errors)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "test_process")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(root, "include"),
+                    os.path.join(root, "tests", "cpp", "test_process.cpp"),
+                    "-L", os.path.join(root, "deoss_amd"), "-ldeoss_merkle",
+                    "-L", os.path.join(root, "oracle"), "-loracle_merkle",   # the checker's restatement only
+                    "-Wl,-rpath," + os.path.join(root, "deoss_amd") + ":" + os.path.join(root, "oracle"),
+                    "-lpthread", "-o", exe], check=True)
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
