@@ -236,6 +236,14 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
 
 int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
     if (!st || (!data && len)) return bad_arg();
+    // fast path: the piece fits the staging slot being filled (no slot wait, no flush): one
+    // memcpy and no HIP call (Go's io.Copy hands over 32 KiB at a time)
+    if (len < kStreamStage - st->fill && !(st->fill == 0 && st->busy[st->slot])) {
+        std::memcpy(st->stage[st->slot].u8() + st->fill, data, len);
+        st->fill += len;
+        st->received += len;
+        return DM_OK;
+    }
     DeviceRestore dev;
     SHIP(hipSetDevice(st->c->devs[st->dev].id));
     const uint8_t* p = static_cast<const uint8_t*>(data);

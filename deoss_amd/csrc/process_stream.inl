@@ -347,9 +347,17 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
 
 int dm_pstream_write(dm_pstream* st, const void* data, uint64_t len) {
     if (!st || (!data && len)) return bad_arg();
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    // fast path (most calls: Go's io.Copy hands over 32 KiB at a time): the piece fits the slot
+    // being filled, so it is one memcpy with no HIP call at all
+    if (st->cur >= 0 && len < st->slot_len - st->fill) {
+        std::memcpy(st->slot[st->cur].u8() + st->fill, p, len);
+        st->fill += len;
+        st->received += len;
+        return DM_OK;
+    }
     DeviceRestore dev;
     PSHIP(hipSetDevice(ps_dev(st).id));
-    const uint8_t* p = static_cast<const uint8_t*>(data);
     while (len) {
         if (st->cur < 0) {
             int rc = ps_drain(st, false);   // parity of coded chunks out first: frees slots early
