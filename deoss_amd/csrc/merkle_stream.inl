@@ -53,6 +53,7 @@ struct dm_stream {
     uint64_t on_device = 0;  // bytes whose H2D is enqueued
     uint64_t launched = 0;   // leaves whose hashing is enqueued
     std::string err;
+    int failed = DM_OK;      // sticky: after a failed write nothing more reaches the GPU; close returns it
 };
 
 namespace {
@@ -181,6 +182,8 @@ void stream_free(dm_stream* st) {
     delete st;
 }
 
+int stream_write(dm_stream* st, const void* data, uint64_t len);
+
 }  // namespace
 
 extern "C" {
@@ -236,6 +239,20 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
 
 int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
     if (!st || (!data && len)) return bad_arg();
+    if (st->failed != DM_OK) {
+        t_err = st->err;
+        return st->failed;
+    }
+    const int rc = stream_write(st, data, len);
+    if (rc != DM_OK) st->failed = rc;
+    return rc;
+}
+
+}  // extern "C"
+
+namespace {
+
+int stream_write(dm_stream* st, const void* data, uint64_t len) {
     // fast path: the piece fits the staging slot being filled (no slot wait, no flush): one
     // memcpy and no HIP call (Go's io.Copy hands over 32 KiB at a time)
     if (len < kStreamStage - st->fill && !(st->fill == 0 && st->busy[st->slot])) {
@@ -266,10 +283,21 @@ int dm_stream_write(dm_stream* st, const void* data, uint64_t len) {
     return DM_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
 const char* dm_stream_error(dm_stream* st) { return st ? st->err.c_str() : ""; }
 
 int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_t* nleaves, uint8_t root[32]) {
     if (!st || !root) return bad_arg();
+    if (st->failed != DM_OK) {   // a write failed: free the stream, report that failure
+        const int rc = st->failed;
+        t_err = st->err;
+        DeviceRestore dev;
+        stream_free(st);
+        return rc;
+    }
     DeviceRestore dev;
     dm_ctx* c = st->c;
     int rc = DM_OK;

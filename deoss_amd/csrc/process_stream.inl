@@ -60,6 +60,7 @@ struct dm_pstream {
     uint64_t drained_upto = 0;      // chunks [0, drained_upto) have their parity written
     std::vector<std::pair<std::string, uint64_t>> pend;   // temporary, digest index (~: segment)
     std::string err;
+    int failed = DM_OK;   // sticky: after a failed write the stream only aborts (close returns this)
 };
 
 namespace {
@@ -283,6 +284,10 @@ void ps_unlink_pending(dm_pstream* st) {
         if (!p.first.empty()) ::unlink(p.first.c_str());
 }
 
+int pstream_write(dm_pstream* st, const void* data, uint64_t len);
+int pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out,
+                  uint8_t fid[32]);
+
 }  // namespace
 
 extern "C" {
@@ -347,6 +352,28 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
 
 int dm_pstream_write(dm_pstream* st, const void* data, uint64_t len) {
     if (!st || (!data && len)) return bad_arg();
+    if (st->failed != DM_OK) return pfail(st, st->failed, st->err);
+    const int rc = pstream_write(st, data, len);
+    if (rc != DM_OK) st->failed = rc;
+    return rc;
+}
+
+int dm_pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out,
+                     uint8_t fid[32]) {
+    if (!st) return bad_arg();
+    if (st->failed != DM_OK) {   // a write failed: nothing of this stream may reach the GPU again
+        const int rc = pfail(st, st->failed, st->err);
+        dm_pstream_abort(st);
+        return rc;
+    }
+    return pstream_close(st, seg_hashes, frag_hashes, cap, nseg_out, fid);
+}
+
+}  // extern "C"
+
+namespace {
+
+int pstream_write(dm_pstream* st, const void* data, uint64_t len) {
     const uint8_t* p = static_cast<const uint8_t*>(data);
     // fast path (most calls: Go's io.Copy hands over 32 KiB at a time): the piece fits the slot
     // being filled, so it is one memcpy with no HIP call at all
@@ -378,9 +405,8 @@ int dm_pstream_write(dm_pstream* st, const void* data, uint64_t len) {
     return DM_OK;
 }
 
-int dm_pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out,
-                     uint8_t fid[32]) {
-    if (!st) return bad_arg();
+int pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out,
+                  uint8_t fid[32]) {
     DeviceRestore dev;
     dm_ctx* c = st->r->c;
     const uint64_t nseg = ceil_div(st->received, st->seg);
@@ -459,6 +485,10 @@ int dm_pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, 
     ps_free(st);
     return rc;
 }
+
+}  // namespace
+
+extern "C" {
 
 void dm_pstream_abort(dm_pstream* st) {
     if (!st) return;

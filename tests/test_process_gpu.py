@@ -501,3 +501,48 @@ def test_cpp_process_mirror(tmp_path):
                     "-lpthread", "-o", exe], check=True)
     r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+def test_processing_stream_write_failure(ctx, tmp_path, monkeypatch):
+    """A savedir the process cannot write: the failure surfaces as DM_ERR_IO with the OS message
+    from a write or from close, the stream stays failed (nothing more reaches the GPU) and no
+    temporary is left.  Needs a non-root user (root writes through mode 0555)."""
+    import ctypes
+    from deoss_amd import DeossMerkleError
+    from oracle import splitmix64_bytes
+    if os.geteuid() == 0:
+        pytest.skip("root ignores directory permissions")
+    monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", "8192")
+    p = _processor(ctx, 4, 8, 4096)
+    ro = tmp_path / "ro"
+    ro.mkdir()
+    ro.chmod(0o555)
+    data = splitmix64_bytes(40 * 4096, 0xDE0552600)
+    L = p.ctx._L
+    h = ctypes.c_void_p()
+    assert L.dm_pstream_open(p.enc._h, 4096, os.fsencode(str(ro)), 1, ctypes.byref(h)) == 0
+    rcs = [L.dm_pstream_write(h, data[i:i + 4096], 4096) for i in range(0, len(data), 4096)]
+    failed = [rc for rc in rcs if rc != 0]
+    if failed:   # sticky: every write after the first failure returns the same code
+        first = rcs.index(failed[0])
+        assert all(rc == failed[0] for rc in rcs[first:])
+    seg = ctypes.create_string_buffer(32 * 64)
+    frag = ctypes.create_string_buffer(32 * 64 * 12)
+    fid = ctypes.create_string_buffer(32)
+    n = ctypes.c_uint64()
+    rc = L.dm_pstream_close(h, seg, frag, 64, ctypes.byref(n), fid)
+    assert rc == -6 and "permission denied" in (L.dm_last_error(None) or b"").decode()
+    assert os.listdir(ro) == []
+    ro.chmod(0o755)
+    # the mirror raises on the same failure and the Processor keeps working
+    ro.chmod(0o555)
+    with pytest.raises(DeossMerkleError, match="permission denied"):
+        st = p.NewProcessingStream(str(ro))
+        for i in range(0, len(data), 4096):
+            st.write(data[i:i + 4096])
+        st.close()
+    ro.chmod(0o755)
+    st = p.NewProcessingStream(str(tmp_path / "ok"))
+    st.write(data)
+    assert len(st.close()[0]) == 40
+    p.close()
