@@ -36,6 +36,7 @@ import (
 	"runtime"
 	"strconv"
 	"sync"
+	"sync/atomic"
 	"unsafe"
 
 	"github.com/CESSProject/cess-go-sdk/chain"
@@ -55,6 +56,8 @@ var (
 	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
 	bufs    sync.Pool     // *windowBuf, reused across calls
 	pipes   chan *C.dm_rs // large files: one dm_full_processing pipeline per GPU
+	coders  []*C.dm_rs    // the same pipelines, for streams (NewWriter picks one round robin)
+	nextW   atomic.Uint64
 	// writeSegments: SegmentHash paths exist as files (the zero-padded segment bytes), like the
 	// fragment paths; DEOSS_SKIP_SEGMENT_FILES=1 skips them (DeOSS itself only opens fragments).
 	writeSegments = os.Getenv("DEOSS_SKIP_SEGMENT_FILES") != "1"
@@ -96,6 +99,7 @@ func gpu() error {
 				return
 			}
 			pipes <- rs
+			coders = append(coders, rs)
 		}
 		// every visible GPU, 2 worker slots each, 4096 leaves per batch, 2 ms linger (DESIGN.md §6.9)
 		if rc := C.dm_batcher_create(nil, 0, C.DM_BATCH_PROCESS, C.uint64_t(chain.SegmentSize), C.int(chain.DataShards),

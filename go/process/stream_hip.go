@@ -37,8 +37,9 @@ func NewWriter(savedir string) (*Writer, error) {
 	if err := gpu(); err != nil {
 		return nil, err
 	}
-	rs := <-pipes // one per GPU; the stream keeps its own streams and buffers, so return it now
-	pipes <- rs
+	// a stream keeps its own HIP streams and buffers and only briefly locks its coder's context at
+	// Close, so it shares the per-GPU pipelines round robin instead of holding one
+	rs := coders[nextW.Add(1)%uint64(len(coders))]
 	cdir := C.CString(savedir)
 	defer C.free(unsafe.Pointer(cdir))
 	flags := C.int(C.DM_FP_SEGMENT_FILES)
