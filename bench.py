@@ -395,7 +395,8 @@ def _summary(r):
     for k in ("n_gpus", "scaling"):
         if k in r:
             keep[k] = r[k]
-    for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel", "cpu", "gpu"):
+    for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel", "cpu", "gpu", "streamed", "after_file_saved",
+              "at_10GbE"):
         if k in r:
             keep[k] = r[k]
     if "leaf_kernel" in r.get("config", {}):
@@ -444,6 +445,8 @@ def driver_extras(args, torch, dist, device, dev_index):
         ("reed_solomon_4+8", run_rs, dict(workload="rs", object_gib=8.0, steps=3, warmup=1, no_cpu=True)),
         ("FullProcessing_file", run_fullprocessing, dict(workload="fullprocessing", object_gib=2.0, steps=2,
                                                          warmup=1, no_cpu=True)),
+        ("FullProcessing_while_receiving", run_process_upload, dict(workload="process_upload", object_gib=2.0,
+                                                                    piece_kib=1024, steps=2, warmup=1)),
     ]
     res = {}
     for name, fn, kw in specs:
