@@ -315,5 +315,8 @@ def FullProcessing(file: str, cipher: str, savedir: str
     """process.FullProcessing(file, cipher, savedir) on the default GPU pipeline."""
     global _default
     if _default is None:
-        _default = Processor()
+        try:
+            _default = Processor()
+        except DeossMerkleError as e:   # no GPU: the Go shape (nil, "", err), as gpu() fails in Go
+            return None, "", e
     return _default.FullProcessing(file, cipher, savedir)

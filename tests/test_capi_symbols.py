@@ -66,3 +66,9 @@ def test_no_gpu_fails_loudly(lib):
     from deoss_amd import DeossMerkleError, MerkleContext
     with pytest.raises(DeossMerkleError):
         MerkleContext()
+    # the FullProcessing mirrors (file form and streaming form) fail the same way
+    from deoss_amd.process import FullProcessing, Processor
+    with pytest.raises(DeossMerkleError):
+        Processor()
+    info, fid, err = FullProcessing(__file__, "", "/nonexistent-savedir")
+    assert info is None and fid == "" and isinstance(err, DeossMerkleError)
