@@ -16,6 +16,7 @@ import argparse
 import hashlib
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -1029,6 +1030,19 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
             list(ex.map(wr, range(nseg * total + nseg)))
         t_io = time.perf_counter() - t0
         fresh()
+        # the host file-I/O floor in C (tools/io_floor.c): read the file with 4 threads and write
+        # the same files with 16 (dm_full_processing's reader / writer counts), nothing else
+        floor = None
+        exe = os.path.join(ROOT, "tools", "io_floor")
+        if not os.path.exists(exe):
+            subprocess.run(["gcc", "-O2", "-pthread", "-o", exe, exe + ".c"], check=False)
+        if os.path.exists(exe):
+            os.makedirs(savedir)
+            r = subprocess.run([exe, path, savedir, str(frag), str(nseg * total), str(seg), str(nseg), "4", "16"],
+                               capture_output=True, text=True)
+            if r.returncode == 0:
+                floor = float(r.stdout.strip())
+            fresh()
         k_avg = k_sum / max(n_t, 1)
         out = {
             "metric": "GiB/s of a file through FullProcessing(file, \"\", savedir): file -> fragment + segment files, fid",
@@ -1043,6 +1057,11 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
             "leaf_kernel_avg_ms": round(k_avg, 3),
             "window_path": {"GiBps": round(length / t_win / (1 << 30), 4), "ms": round(t_win * 1e3, 1),
                             "what": "read 8 segments, dm_process_buffer, write their files from Python, repeat"},
+            "host_io_floor": None if floor is None else {
+                "GiBps": round(length / floor / (1 << 30), 4), "ms": round(floor * 1e3, 1),
+                "frac_of_floor": round(floor / tavg, 4),
+                "what": f"tools/io_floor.c: read {length} B (4 threads) + write {out_bytes} B as the same files "
+                        "(16 threads); no hashing, coding or GPU"},
             "python_io_only": {"GiBps": round(length / t_io / (1 << 30), 4), "ms": round(t_io * 1e3, 1),
                                "what": f"read {length} B + write {out_bytes} B as the same number of files from "
                                        "Python, 16 threads, no hashing or coding (a host-side reference point)"},
