@@ -125,12 +125,13 @@ bool read_part(const FileSet& fs, const FilePart& p, std::string* err) {
 
 constexpr int kReaders = 4;   // pread threads per device (page-cache copies run ~5-10 GB/s each)
 
-// Read every part, up to kReaders threads; on failure the lowest failing file wins (Go's order).
-int read_parts(dm_ctx* c, const FileSet& fs, const std::vector<FilePart>& parts) {
+// Read every part, up to `readers` threads; on failure the lowest failing file wins (Go's order).
+int read_parts(dm_ctx* c, const FileSet& fs, const std::vector<FilePart>& parts, int readers = kReaders) {
     if (parts.empty()) return DM_OK;
     uint64_t bytes = 0;
     for (const auto& p : parts) bytes += p.len;
-    const int R = (int)std::min<uint64_t>(kReaders, std::max<uint64_t>(1, std::min<uint64_t>(parts.size(), bytes >> 22)));
+    const int R = (int)std::min<uint64_t>((uint64_t)readers,
+                                          std::max<uint64_t>(1, std::min<uint64_t>(parts.size(), bytes >> 22)));
     std::vector<uint64_t> bad(R, ~0ull);
     std::vector<std::string> msg(R);
     auto run = [&](int t) {

@@ -4,14 +4,15 @@
 // in one call.  Part of merkle_capi.hip (after files_capi.inl, rs_capi.inl, process_capi.inl).
 //
 // Per window of segments (up to kFpWindowBytes of file; one window up to 32 GiB):
-//   A. the file is pread into pinned slots (whole segments per slot, parallel readers); each slot
-//      is copied to HBM, and its data fragments -- plain file bytes, so their contents are known
-//      already -- are written to temporary files by background writers while the next slot is
-//      read (the last segment's zero padding is filled in the slot);
+//   A. the file is pread into pinned slots (whole segments per slot, parallel readers) and each
+//      slot is copied to HBM -- nothing else, so the leaf chains can start as soon as the reads
+//      allow (the last segment's zero padding is filled in the slot);
 //   B. one RS launch and one leaf launch over the window's segments and fragments
 //      (process_segments, the same GPU pass as dm_process_buffer);
-//   C. while the leaf kernel's serial chains run (~0.5 s for 32 MiB segments), the parity
-//      fragments come back through the same slots and are written to temporary files;
+//   C. while the leaf kernel's serial chains run (~0.5 s for 32 MiB segments), the data fragments
+//      and segment files -- plain file bytes -- are copied from the file by background writers
+//      (copy_file_range, page cache to page cache), and the parity fragments come back through
+//      the slots and are written to temporary files;
 //   D. the digests come back and every temporary file is renamed to savedir/<hex SHA-256>.
 // The fid is the hashtree root over all segment digests.  The Go shim's window path (read a
 // window, one batched GPU call, then write its fragments) leaves the GPU idle during the writes
@@ -21,10 +22,30 @@ namespace {
 
 constexpr uint64_t kFpSlotBytes = 64ull << 20;         // pinned slot (whole segments / parity sets)
 constexpr int kFpSlots = 4;                             // = dm_rs::fp_slot
-constexpr int kFpWritersPerSlot = 4;                    // background write jobs per slot
+constexpr int kFpWritersPerSlot = 4;                    // background write jobs per parity slot
+constexpr size_t kFpDataWriters = 8;                    // jobs copying data fragments / segments from the file
+constexpr int kFpReaders = 8;                           // pread threads per slot (phase A gates the leaf pass)
+
+struct FdGuard {
+    int fd = -1;
+    ~FdGuard() {
+        if (fd >= 0) ::close(fd);
+    }
+};
 constexpr uint64_t kFpWindowBytes = 32ull << 30;        // file bytes per GPU pass (+ 2x parity in HBM)
 
 std::atomic<uint64_t> g_fp_seq{0};
+
+// DEOSS_FP_TRACE=1: phase times of each dm_full_processing window on stderr (diagnostics)
+struct FpTrace {
+    bool on = std::getenv("DEOSS_FP_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(const char* what) const {
+        if (on)
+            std::fprintf(stderr, "[fp] %-28s %8.1f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
 
 uint64_t env_bytes(const char* name, uint64_t dflt) {
     const char* v = std::getenv(name);
@@ -76,23 +97,73 @@ std::string mkdir_all(const std::string& dir) {
     return "";
 }
 
-struct FpFile {          // one file to write: bytes, temporary name, and where its digest will be
+struct FpFile {          // one file to write: its bytes (memory, or a range of an open file) and temporary name
     const uint8_t* src;
     uint64_t len;
     std::string tmp;
+    int in_fd = -1;         // >= 0: the bytes are [in_off, in_off + len) of this file (copied in the kernel)
+    uint64_t in_off = 0;
 };
+
+// A file range into a new file: copy_file_range (page cache to page cache in the kernel, no user
+// copy), or pread / write through a bounce buffer where the kernel cannot.
+std::string copy_whole(const std::string& path, int in_fd, uint64_t off, uint64_t len) {
+    const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0777);
+    if (fd < 0) return "open " + path + ": " + go_errno(errno);
+    uint64_t done = 0;
+    bool kernel = true;
+    std::vector<uint8_t> bounce;
+    while (done < len) {
+        if (kernel) {
+            loff_t io = (loff_t)(off + done);
+            const ssize_t w = ::copy_file_range(in_fd, &io, fd, nullptr, len - done, 0);
+            if (w > 0) {
+                done += (uint64_t)w;
+                continue;
+            }
+            if (w < 0 && errno == EINTR) continue;
+            if (w < 0 && errno != EXDEV && errno != ENOSYS && errno != EINVAL && errno != EOPNOTSUPP) {
+                const int e = errno;
+                ::close(fd);
+                return "write " + path + ": " + go_errno(e);
+            }
+            kernel = false;   // 0 (short source) or unsupported: finish through user space
+            bounce.resize(8ull << 20);
+        }
+        const uint64_t n = std::min<uint64_t>(bounce.size(), len - done);
+        const ssize_t r = ::pread(in_fd, bounce.data(), n, (off_t)(off + done));
+        if (r <= 0) {
+            ::close(fd);
+            return "read: " + (r < 0 ? go_errno(errno) : std::string("unexpected EOF"));
+        }
+        for (ssize_t put = 0; put < r;) {
+            const ssize_t w = ::write(fd, bounce.data() + put, (size_t)(r - put));
+            if (w < 0 && errno == EINTR) continue;
+            if (w <= 0) {
+                const int e = w < 0 ? errno : EIO;
+                ::close(fd);
+                return "write " + path + ": " + go_errno(e);
+            }
+            put += w;
+        }
+        done += (uint64_t)r;
+    }
+    if (::close(fd) != 0) return "close " + path + ": " + go_errno(errno);
+    return "";
+}
 
 // Background writes out of one pinned slot; wait() joins them before the slot is refilled.
 struct SlotWrites {
     std::vector<std::future<std::string>> jobs;
-    void start(std::vector<FpFile> files) {
-        const size_t J = std::min<size_t>(kFpWritersPerSlot, files.size());
+    void start(std::vector<FpFile> files, size_t jobs_max = kFpWritersPerSlot) {
+        const size_t J = std::min<size_t>(jobs_max, files.size());
         for (size_t j = 0; j < J; j++) {
             std::vector<FpFile> mine;
             for (size_t i = j; i < files.size(); i += J) mine.push_back(files[i]);
             jobs.push_back(std::async(std::launch::async, [mine]() {
                 for (const auto& f : mine) {
-                    std::string e = write_whole(f.tmp, f.src, f.len);
+                    std::string e = f.in_fd >= 0 ? copy_whole(f.tmp, f.in_fd, f.in_off, f.len)
+                                                 : write_whole(f.tmp, f.src, f.len);
                     if (!e.empty()) return e;
                 }
                 return std::string();
@@ -146,6 +217,17 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
     HIP_TRY(hipEventCreateWithFlags(&ev.copied, hipEventDisableTiming));
     const std::string base = dir + "/.dm-fp-" + std::to_string((long long)::getpid()) + "-" +
                              std::to_string((unsigned long long)g_fp_seq++) + "-";
+    // where data files are copied from: the open file (kernel copies) or, for a pipe, its bytes
+    const uint8_t* mem = fs.mem[0].empty() ? nullptr : fs.mem[0].data();
+    int in_fd = fs.fd[0];
+    FdGuard own_fd;
+    if (!mem && in_fd < 0) {
+        in_fd = own_fd.fd = ::open(fs.path[0].c_str(), O_RDONLY | O_CLOEXEC);
+        if (in_fd < 0) return fail(c, DM_ERR_IO, "open %s: %s", fs.path[0].c_str(), go_errno(errno).c_str());
+    }
+    std::vector<uint8_t> tail;      // the zero-padded last segment (its data files are written from here)
+    uint64_t tail_seg = ~0ull;
+    SlotWrites wd;                  // data-fragment / segment-file writers (declared after their sources)
     SlotWrites wr[kFpSlots];
     bool busy[kFpSlots] = {false, false, false, false};
     uint64_t next = 0;   // slot round robin across both phases and windows
@@ -161,6 +243,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         return DM_OK;
     };
     const bool one_window = nseg <= win;
+    FpTrace tr;
     for (uint64_t w0 = 0; w0 < nseg; w0 += win) {
         const uint64_t ns = std::min(win, nseg - w0);
         const uint64_t fbeg = w0 * seg, fend = std::min(size, (w0 + ns) * seg);
@@ -168,7 +251,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         HIP_TRY(r->work.ensure(ns * pbytes + 32));
         uint8_t* parity = r->work.u8();
         uint8_t* dfid = parity + ns * pbytes;
-        // A: file -> slots -> HBM; data fragments (+ segments) written from the slot meanwhile
+        // A: file -> slots -> HBM, nothing else, so the leaf chains start as early as the reads allow
         for (uint64_t t0 = 0; t0 < ns; t0 += spd) {
             const uint64_t nt = std::min(spd, ns - t0), len = nt * seg, a = fbeg + t0 * seg;
             int sl;
@@ -176,34 +259,49 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             uint8_t* buf = r->fp_slot[sl].u8();
             const uint64_t have = a < fend ? std::min(len, fend - a) : 0;
             std::vector<FilePart> parts;
-            for (uint64_t q = 0; q < have; q += 16ull << 20)
-                parts.push_back({0, a + q, std::min<uint64_t>(16ull << 20, have - q), buf + q});
-            RC_TRY(read_parts(c, fs, parts));
+            for (uint64_t q = 0; q < have; q += 8ull << 20)
+                parts.push_back({0, a + q, std::min<uint64_t>(8ull << 20, have - q), buf + q});
+            RC_TRY(read_parts(c, fs, parts, kFpReaders));
             if (have < len) std::memset(buf + have, 0, len - have);
             HIP_TRY(hipMemcpyAsync(d.data.u8() + t0 * seg, buf, len, hipMemcpyHostToDevice, d.copy));
             HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
-            std::vector<FpFile> files;
-            for (uint64_t u = 0; u < nt; u++) {
-                const uint64_t gs = w0 + t0 + u;
-                for (int j = 0; j < k; j++) {
-                    const uint64_t id = gs * (uint64_t)total + (uint64_t)j;
-                    files.push_back({buf + u * seg + (uint64_t)j * frag, frag, base + "f" + std::to_string(id)});
-                    pend.emplace_back(files.back().tmp, 32 * id);
-                }
-                if (flags & DM_FP_SEGMENT_FILES) {
-                    files.push_back({buf + u * seg, seg, base + "s" + std::to_string(gs)});
-                    pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
-                }
-            }
-            wr[sl].start(std::move(files));
             busy[sl] = true;
+            if (t0 + nt == ns && have < len) {   // the file's last, zero-padded segment: keep a copy
+                tail.assign(buf + (nt - 1) * seg, buf + nt * seg);
+                tail_seg = w0 + t0 + nt - 1;
+            }
         }
+        tr.mark("A: reads + H2D enqueued");
         // B: RS + one leaf launch over segments and fragments, after the last H2D
         HIP_TRY(hipEventRecord(ev.copied, d.copy));
         HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
         RC_TRY(process_segments(r, d, s, d.data.u8(), seg, parity, {0, ns}, dfid, ev.rs));
-        // C: parity back through the slots while the leaf chains run; written as each set lands
+        // C: while the leaf chains run, the data fragments and segment files are copied from the
+        // file itself (copy_file_range: page cache to page cache), and the parity comes back
+        // through the slots and is written as each set lands
+        {
+            std::vector<FpFile> files;
+            for (uint64_t gs = w0; gs < w0 + ns; gs++) {
+                const bool padded = gs == tail_seg;
+                auto add = [&](uint64_t off_in_seg, uint64_t len, const std::string& tmp) {
+                    if (padded) files.push_back({tail.data() + off_in_seg, len, tmp});
+                    else if (mem) files.push_back({mem + gs * seg + off_in_seg, len, tmp});
+                    else files.push_back({nullptr, len, tmp, in_fd, gs * seg + off_in_seg});
+                };
+                for (int j = 0; j < k; j++) {
+                    const uint64_t id = gs * (uint64_t)total + (uint64_t)j;
+                    add((uint64_t)j * frag, frag, base + "f" + std::to_string(id));
+                    pend.emplace_back(files.back().tmp, 32 * id);
+                }
+                if (flags & DM_FP_SEGMENT_FILES) {
+                    add(0, seg, base + "s" + std::to_string(gs));
+                    pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
+                }
+            }
+            wd.start(std::move(files), kFpDataWriters);
+        }
         HIP_TRY(hipStreamWaitEvent(d.copy, ev.rs, 0));
+        tr.mark("B: launched, data copies started");
         for (uint64_t t0 = 0; t0 < ns; t0 += spp) {
             const uint64_t nt = std::min(spp, ns - t0);
             int sl;
@@ -224,6 +322,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             wr[sl].start(std::move(files));
             busy[sl] = true;
         }
+        tr.mark("C: parity back, writes queued");
         // D: digests (d.leaves: segment t at t, fragment (t, j) at ns + t * total + j)
         HIP_TRY(hipMemcpyAsync(segd.data() + 32 * w0, d.leaves.p, 32 * ns, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(fragd.data() + 32 * w0 * total, d.leaves.u8() + 32 * ns, 32 * ns * total,
@@ -231,11 +330,16 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         if (one_window) HIP_TRY(hipMemcpyAsync(fid, dfid, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipStreamSynchronize(d.copy));   // this window's slots are in host memory: HBM reusable
+        tr.mark("D: leaf pass done");
+        const std::string e = wd.wait();
+        tr.mark("data files written");   // the window's data files, before the next window reuses `tail`
+        if (!e.empty()) return fail(c, DM_ERR_IO, "%s", e.c_str());
     }
     for (int sl = 0; sl < kFpSlots; sl++) {
         const std::string e = wr[sl].wait();
         if (!e.empty()) return fail(c, DM_ERR_IO, "%s", e.c_str());
     }
+    tr.mark("parity files written");
     if (!one_window) {   // several windows: the fid is the tree over every segment digest
         HIP_TRY(d.leaves.ensure(32 * nseg));
         HIP_TRY(hipMemcpyAsync(d.leaves.p, segd.data(), 32 * nseg, hipMemcpyHostToDevice, s));
