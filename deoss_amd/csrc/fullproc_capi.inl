@@ -298,7 +298,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
                     pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
                 }
             }
-            wd.start(std::move(files), kFpDataWriters);
+            wd.start(std::move(files), (size_t)env_bytes("DEOSS_FP_DATA_WRITERS", kFpDataWriters));
         }
         HIP_TRY(hipStreamWaitEvent(d.copy, ev.rs, 0));
         tr.mark("B: launched, data copies started");
