@@ -38,6 +38,12 @@ FRAGMENT_SIZE = SEGMENT_SIZE // DATA_SHARDS   # chain.FragmentSize (8 MiB; node/
 WINDOW_SEGMENTS = 8                           # segments per GPU call (256 MiB of file + 768 MiB of fragments; the Go shim bounds windows in flight by DEOSS_PROCESS_MEM_GIB)
 
 
+def _write_segments() -> bool:
+    """Segment files are written unless DEOSS_SKIP_SEGMENT_FILES=1 (as in the Go shim: DeOSS itself
+    only opens fragment paths, node/fileHandler.go:967-969)."""
+    return os.environ.get("DEOSS_SKIP_SEGMENT_FILES") != "1"
+
+
 @dataclass
 class SegmentDataInfo:
     """chain.SegmentDataInfo: the segment's path name and its fragments' path names."""
@@ -127,11 +133,13 @@ class Processor:
                                                         stream), "dm_process_device_async")
 
     # -- FullProcessing ----------------------------------------------------------------------------
-    def full_processing_file(self, file: str, savedir: str, segment_files: bool = True
+    def full_processing_file(self, file: str, savedir: str, segment_files: Optional[bool] = None
                              ) -> Tuple[bytes, bytes, bytes]:
         """One ``dm_full_processing`` call: the library reads ``file``, writes every fragment (and
         segment) to ``savedir/<hex SHA-256>`` and returns (segment digests, fragment digests, fid)."""
         L = self.ctx._L
+        if segment_files is None:
+            segment_files = _write_segments()
         try:
             size = os.stat(file).st_size
         except OSError:
@@ -173,7 +181,7 @@ class Processor:
             info.append(SegmentDataInfo(os.path.join(savedir, segd[32 * s:32 * s + 32].hex()), names))
         return info, fid.hex(), None
 
-    def NewProcessingStream(self, savedir: str, segment_files: bool = True) -> "ProcessingStream":
+    def NewProcessingStream(self, savedir: str, segment_files: Optional[bool] = None) -> "ProcessingStream":
         """FullProcessing while the body arrives: write() the pieces, close() -> (info, fid)."""
         return ProcessingStream(self, savedir, segment_files)
 
@@ -232,12 +240,14 @@ class ProcessingStream:
     every fragment and segment file in ``savedir`` -- the same results as
     ``FullProcessing(file, "", savedir)`` on the same bytes, without reading the file again."""
 
-    def __init__(self, proc: "Processor", savedir: str, segment_files: bool = True):
+    def __init__(self, proc: "Processor", savedir: str, segment_files: Optional[bool] = None):
         self._p = proc
         self._L = proc.ctx._L
         self.savedir = savedir
         self.written = 0
         h = ctypes.c_void_p()
+        if segment_files is None:
+            segment_files = _write_segments()
         rc = self._L.dm_pstream_open(proc.enc._h, proc.segment, os.fsencode(savedir), 1 if segment_files else 0,
                                      ctypes.byref(h))
         self._raise(rc, "dm_pstream_open")
