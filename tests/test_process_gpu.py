@@ -546,3 +546,24 @@ def test_processing_stream_write_failure(ctx, tmp_path, monkeypatch):
     st.write(data)
     assert len(st.close()[0]) == 40
     p.close()
+
+
+def test_skip_segment_files(ctx, oracle_lib, tmp_path, monkeypatch):
+    """DEOSS_SKIP_SEGMENT_FILES=1 (Go, C++ and Python shims alike): only fragment files are written,
+    digests and fid unchanged; file form and streaming form."""
+    from oracle import splitmix64_bytes
+    monkeypatch.setenv("DEOSS_SKIP_SEGMENT_FILES", "1")
+    p = _processor(ctx, 4, 8, 4096)
+    data = splitmix64_bytes(5 * 4096 + 77, 0xDE0552700)
+    f = tmp_path / "obj.bin"
+    f.write_bytes(data)
+    seg_b, frag_b, want_fid, _ = oracle_lib.full_processing(data, 4096, 4, 8)
+    frag_names = {frag_b[i:i + 32].hex() for i in range(0, len(frag_b), 32)}
+    segd, fragd, fid = p.full_processing_file(str(f), str(tmp_path / "a"))
+    assert (segd, fragd, fid) == (seg_b, frag_b, want_fid)
+    assert set(os.listdir(tmp_path / "a")) == frag_names
+    st = p.NewProcessingStream(str(tmp_path / "b"))
+    st.write(data)
+    assert st.close()[1] == want_fid.hex()
+    assert set(os.listdir(tmp_path / "b")) == frag_names
+    p.close()
