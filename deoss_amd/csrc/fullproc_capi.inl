@@ -209,6 +209,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
     const uint64_t spp = std::max<uint64_t>(1, slot_bytes / pbytes);         // segments per parity slot
     const uint64_t slot_cap = std::max(spd * seg, spp * pbytes);
     const uint64_t win = std::max<uint64_t>(spd, window_bytes / seg / spd * spd);   // segments per window
+    const int readers = (int)std::min<uint64_t>(64, env_bytes("DEOSS_FP_READERS", kFpReaders));
     RC_TRY(begin_call(c, d, s));
     for (auto& b : r->fp_slot) HIP_TRY(b.ensure(slot_cap));
     FpEvents ev;
@@ -261,7 +262,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             std::vector<FilePart> parts;
             for (uint64_t q = 0; q < have; q += 8ull << 20)
                 parts.push_back({0, a + q, std::min<uint64_t>(8ull << 20, have - q), buf + q});
-            RC_TRY(read_parts(c, fs, parts, kFpReaders));
+            RC_TRY(read_parts(c, fs, parts, readers));
             if (have < len) std::memset(buf + have, 0, len - have);
             HIP_TRY(hipMemcpyAsync(d.data.u8() + t0 * seg, buf, len, hipMemcpyHostToDevice, d.copy));
             HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
