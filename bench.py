@@ -35,6 +35,59 @@ def env_int(name, default):
     return int(v) if v not in (None, "") else default
 
 
+def host_cpu_facts() -> dict:
+    """What the CPU baseline ran on: model, sockets, physical cores, logical CPUs, this process's
+    affinity, the cgroup CPU quota and the share the job may use ("report nproc and
+    the model").  The GPU box shows the whole machine in os.cpu_count() but allots 16 CPUs per GPU
+    (OMP_NUM_THREADS / MAX_JOBS are set to that share there), so worker pools use `share`."""
+    model, phys, sockets = None, set(), set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as f:
+            for line in list(f) + ["\n"]:
+                if not line.strip():
+                    if "physical id" in cur:
+                        sockets.add(cur["physical id"])
+                        phys.add((cur["physical id"], cur.get("core id", cur.get("processor"))))
+                    cur = {}
+                    continue
+                k, _, v = line.partition(":")
+                cur[k.strip()] = v.strip()
+                if k.strip() == "model name" and model is None:
+                    model = v.strip()
+    except OSError:
+        pass
+    logical = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = logical
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    share = affinity
+    if quota:
+        share = min(share, max(1, int(quota)))
+    for var in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(var)
+        if v and v.isdigit() and int(v) > 0:
+            share = min(share, int(v))
+            break
+    return {"model": model, "sockets": len(sockets) or None, "physical_cores": len(phys) or None,
+            "logical_cpus": logical, "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "share": share,
+            "share_basis": "min(affinity, cgroup quota, OMP_NUM_THREADS/MAX_JOBS): the CPUs this job may use"}
+
+
+def cpu_share() -> int:
+    """Worker threads for CPU checkers and the parallel baseline: this job's CPU share."""
+    return max(1, host_cpu_facts()["share"])
+
+
 def blocks_for(length: int, chunk: int) -> int:
     """Compression blocks of the whole tree: sum ceil((len+9)/64) + 2 x nodes."""
     n = (length + chunk - 1) // chunk
@@ -334,8 +387,12 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         par = out.get("cpu_baseline", {}).get("parallel")
         if par and par.get("value"):
             out["vs_baseline"] = round(value / par["value"], 4)
-            out["vs_baseline_basis"] = (f"GPU value / the {par['cores']}-thread CPU restatement on this host, same "
-                                        "object, same run (BASELINE.md publishes no reference number)")
+            out["vs_baseline_basis"] = (f"GPU value / the {par['cores']}-thread CPU restatement on this host (the "
+                                        "job's CPU share), same object, same run (BASELINE.md publishes no "
+                                        "reference number)")
+            est = out["cpu_baseline"].get("all_physical_cores_estimate", {})
+            if est.get("value"):
+                out["vs_all_physical_cores_estimate"] = round(value / est["value"], 4)
     if world > 1 and not args.no_verify:
         out["parity"] = multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, chunk,
                                           root_hex, barrier, gloo)
@@ -391,7 +448,7 @@ def _summary(r):
     keep["workload"] = r.get("config", {}).get("workload")
     par = r.get("parity", {})
     keep["bit_exact"] = par.get("bit_exact")
-    if "prefix_bit_exact" in par or "ranks" in par:
+    if "prefix_bit_exact" in par or "ranks" in par or "checked_objects" in par:
         keep["parity"] = par
     for k in ("n_gpus", "scaling"):
         if k in r:
@@ -515,7 +572,7 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
         if not args.no_cpu:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             from oracle import Oracle
-            threads = max(1, min(os.cpu_count() or 1, 16 * (1 if args.same_device else world)))   # box CPU share
+            threads = max(1, min(os.cpu_count() or 1, cpu_share() * (1 if args.same_device else world)))   # job CPU share
             t0 = time.perf_counter()
             _, cr = Oracle().root_synthetic(total, chunk, SEED, nthreads=threads)
             dt = time.perf_counter() - t0
@@ -570,7 +627,7 @@ def run_files(args, torch, dist, world, rank, device, dev_index, gloo):
             leaves, root = ctx.new_hash_tree(paths)
             times.append(time.perf_counter() - t0)
         tavg = sum(times) / len(times)
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_share()
         want_leaves, want = orc.root_synthetic(total, size, SEED, nthreads=threads, want_leaves=True)
         parity = {"root": root.hex(), "cpu_root": want.hex(),
                   "bit_exact": root == want and b"".join(leaves) == want_leaves}
@@ -684,7 +741,7 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         root, t, tail = one()
         times.append(t)
         tails.append(tail)
-    _, want = orc.root_buffer_ptr(base, length, chunk, nthreads=min(16, os.cpu_count() or 1))
+    _, want = orc.root_buffer_ptr(base, length, chunk, nthreads=cpu_share())
     tavg = sum(times) / len(times)
     out = {
         "metric": "host-buffer upload GiB/s hashed to Merkle root while receiving (dm_stream, pageable pieces)",
@@ -764,7 +821,7 @@ def run_rs(args, torch, dist, world, rank, device, dev_index, gloo):
     for s_i in sorted({0, nseg - 1}):
         d = data[s_i * seg:(s_i + 1) * seg].cpu().numpy()
         want = orc.rs_encode([d[j * shard:(j + 1) * shard].tobytes() for j in range(4)], 8,
-                             nthreads=min(16, os.cpu_count() or 1))
+                             nthreads=cpu_share())
         got = parity[s_i * 2 * seg:(s_i + 1) * 2 * seg].cpu().numpy()
         same = all(got[i * shard:(i + 1) * shard].tobytes() == want[i] for i in range(8))
         checked.append(s_i)
@@ -800,7 +857,7 @@ def run_rs(args, torch, dist, world, rank, device, dev_index, gloo):
         outs = [ctypes.create_string_buffer(shard) for _ in range(8)]
         pp = [ctypes.addressof(b) for b in outs]
         res = {}
-        for threads in (1, min(16, os.cpu_count() or 1)):
+        for threads in (1, cpu_share()):
             t0 = time.perf_counter()
             for s_i in range(sample):
                 orc.rs_encode_ptrs(4, 8, [buf + s_i * seg + j * shard for j in range(4)], pp, shard, threads)
@@ -873,7 +930,7 @@ def run_process(args, torch, dist, world, rank, device, dev_index, gloo):
     # fragment digests of the first and last segment (CPU restatement of Split + Encode + SHA-256)
     orc = Oracle()
     host = obj[:length].cpu().numpy()
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_share()
     padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
     want_seg, _ = orc.root_buffer_ptr(host.ctypes.data, (nseg - 1) * seg, seg, threads, True) if nseg > 1 \
         else (b"", None)
@@ -984,7 +1041,7 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
         # their bytes for a sample, exactly the expected set, no temporary left)
         import numpy as np
         host = np.fromfile(path, dtype=np.uint8)
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_share()
         padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
         want_seg = orc.root_buffer_ptr(host.ctypes.data, (nseg - 1) * seg, seg, threads, True)[0] if nseg > 1 else b""
         want_seg = (want_seg or b"") + orc.sha256(padded)
@@ -1172,7 +1229,7 @@ def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         st = res["streamed"][-1][3]
         segd, fragd = res["after"][-1][3]
         # parity: streamed = file form (every digest, the fid); segment digests + fid vs the CPU
-        threads = min(16, os.cpu_count() or 1)
+        threads = cpu_share()
         host = body.numpy()
         padded = host[(nseg - 1) * seg:].tobytes() + bytes(nseg * seg - length)
         want_seg = orc.root_buffer_ptr(addr, (nseg - 1) * seg, seg, threads, True)[0] if nseg > 1 else b""
@@ -1254,7 +1311,7 @@ def run_proofs(args, torch, dist, world, rank, device, dev_index, gloo):
     all_ok = int(ok.sum().item()) == n
     orc = Oracle()
     host = obj.cpu().numpy()
-    _, want_root = orc.root_buffer_ptr(host.ctypes.data, n * leaf, leaf, min(16, os.cpu_count() or 1))
+    _, want_root = orc.root_buffer_ptr(host.ctypes.data, n * leaf, leaf, cpu_share())
     root_ok = bytes(root.cpu().numpy()) == want_root and bytes(nodes[-32:].cpu().numpy()) == want_root
     if rank != 0:
         return
@@ -1461,19 +1518,31 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     got = last if args.workload == "stream" else bytes(roots.cpu().numpy())
-    # parity: every root of this rank against the CPU oracle (16 threads, untimed)
+    # parity: EVERY root of this rank against the CPU oracle (the job's CPU share, untimed).  The
+    # device-resident objects are copied back once and hashed from host memory; the generator
+    # itself is checked on a sample of objects against the oracle's independent splitmix64.
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import Oracle
     orc = Oracle()
-    src = host if host is not None else None
-    mism = 0
-    check = min(nobj, 512)
-    for j in range(check):
-        if src is not None:
-            addr = src.data_ptr() + j * pitch
-            _, want = orc.root_buffer_ptr(addr, obj, chunk, nthreads=1)
-        else:
-            want = orc.root_buffer(orc.splitmix_bytes(obj, seed0 + j), chunk)[1]
-        mism += want != got[32 * j:32 * j + 32]
+    gen_checked = gen_bad = 0
+    if host is None:
+        host = torch.empty(pitch * nobj, dtype=torch.uint8, pin_memory=True)
+        host.copy_(buf[:pitch * nobj])
+        torch.cuda.synchronize()
+        del buf
+        hv = host.numpy()
+        for j in sorted({0, nobj // 3, nobj // 2, nobj - 1}):
+            gen_checked += 1
+            gen_bad += bytes(hv[j * pitch:j * pitch + obj]) != orc.splitmix_bytes(obj, seed0 + j)
+    base = host.data_ptr()
+
+    def want_root(j):
+        return orc.root_buffer_ptr(base + j * pitch, obj, chunk, nthreads=1)[1]
+
+    with ThreadPoolExecutor(cpu_share()) as pool:
+        wants = list(pool.map(want_root, range(nobj)))
+    check = nobj
+    mism = sum(wants[j] != got[32 * j:32 * j + 32] for j in range(nobj)) + gen_bad
     leaves = (obj + chunk - 1) // chunk * nobj
     kind = ctx.leaf_kernel_for(leaves)
     out = {
@@ -1491,7 +1560,8 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
                    "objects_per_gpu": nobj, "object_bytes": obj, "chunk": chunk, "leaf_kernel": kind,
                    "parallelism": f"{world} replica(s), objects split across ranks, no exchange"},
         "k1_avg_ms": round(k1_ms_sum / max(ncalls, 1), 4), "call_avg_ms": round(call_ms_sum / max(ncalls, 1), 4),
-        "parity": {"checked_objects": check, "mismatches": int(mism), "bit_exact": mism == 0},
+        "parity": {"checked_objects": check, "objects": nobj, "mismatches": int(mism), "bit_exact": mism == 0,
+                   "generator_sample_checked": gen_checked},
     }
     if args.same_device:
         out.update({"ranks": world, "same_device": True,
@@ -1519,18 +1589,43 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         torch.cuda.synchronize()
     if not args.no_cpu:
         # faithful serial restatement of common/hashtree over the same 8 GiB (1 core, SHA-NI when present)
+        facts = host_cpu_facts()
         t0 = time.perf_counter()
         _, cpu_root = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=1)
         t1 = time.perf_counter()
-        nthr = min(16, os.cpu_count() or 1)
+        nthr = facts["share"]
         _, cpu_root_p = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=nthr)
         t2 = time.perf_counter()
+        half = max(1, nthr // 2)
+        _, cpu_root_h = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=half)
+        t3 = time.perf_counter()
+        serial = length / (t1 - t0) / (1 << 30)
+        par = length / (t2 - t1) / (1 << 30)
+        # Every leaf is one serial chain on one core, so a host with P physical cores hashes the
+        # n leaves in ceil(n / P) rounds of one chain (the per-thread rate measured at the share).
+        n_leaves = (length + chunk - 1) // chunk
+        P = facts["physical_cores"] or facts["logical_cpus"]
+        per_thread = par / nthr
+        rounds_share = -(-n_leaves // nthr)
+        rounds_all = -(-n_leaves // P)
+        est_all = per_thread * nthr * rounds_share / rounds_all if rounds_all else None
         out["cpu_baseline"] = {
-            "value": round(length / (t1 - t0) / (1 << 30), 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "value": round(serial, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": f"the full {length} B object of the timed workload, chunk {chunk}, serial leaves then tree "
                       f"(oracle/merkle_oracle.c, SHA-256 backend {orc.backend()}; stands in for Go crypto/sha256)",
-            "parallel": {"value": round(length / (t2 - t1) / (1 << 30), 4), "cores": nthr},
+            "host": facts,
+            "parallel": {"value": round(par, 4), "cores": nthr,
+                         "scaling": {"1": round(serial, 4), str(half): round(length / (t3 - t2) / (1 << 30), 4),
+                                     str(nthr): round(par, 4)},
+                         "note": "leaves across the job's CPU share (the GPU box allots 16 CPUs per GPU; "
+                                 "os.cpu_count() there is the whole machine)"},
+            "all_physical_cores_estimate": {
+                "value": round(est_all, 4) if est_all else None, "cores": P,
+                "method": f"per-thread rate at the share x min(P, leaves): {n_leaves} leaves in "
+                          f"ceil({n_leaves}/{P}) = {rounds_all} rounds of one chain instead of {rounds_share}; "
+                          "measured, not run: the box's job limits forbid using every core"},
         }
+        cpu_root_p = cpu_root_p if cpu_root_h == cpu_root_p else b"mismatch"
         out["parity"] = {"gpu_root": root_hex, "cpu_root": cpu_root.hex(),
                          "bit_exact": cpu_root.hex() == root_hex and cpu_root_p == cpu_root}
     if do_e2e and host is not None:
@@ -1578,7 +1673,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
                      "k1_gbs": round(length / (k1 / n * 1e-3) / 1e9, 2),
                      "k1_hbm_frac": round(length / (k1 / n * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)}
             if host is not None and not args.no_cpu:
-                _, cr = orc.root_buffer_ptr(host.data_ptr(), length, c, nthreads=min(16, os.cpu_count() or 1))
+                _, cr = orc.root_buffer_ptr(host.data_ptr(), length, c, nthreads=cpu_share())
                 entry["bit_exact"] = cr == gpu_root
             sweep.append(entry)
         ctx.set_leaf_kernel("auto")
