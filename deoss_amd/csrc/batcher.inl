@@ -56,7 +56,7 @@ namespace {
 
 // ROOT batch on one slot context: per-object roots and (optionally) leaf digests.
 int batch_roots_host(dm_ctx* c, const std::vector<BatchReq*>& reqs, uint64_t chunk) {
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     Dev& d = c->devs[0];
     RC_TRY(begin_call(c, d, d.stream));
     const uint64_t n = reqs.size();
@@ -83,7 +83,7 @@ int batch_roots_host(dm_ctx* c, const std::vector<BatchReq*>& reqs, uint64_t chu
 
 int batch_process_host(dm_rs* r, const std::vector<BatchReq*>& reqs, uint64_t segment) {
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     const uint64_t n = reqs.size();
     std::vector<const void*> ptrs(n);
     std::vector<uint64_t> lens(n);

@@ -272,18 +272,29 @@ extern "C" {
 
 int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t* leaf_out, uint8_t root[32]) {
     if (!ctx || !root || (n && !paths)) return bad_arg();
-    CallLock lk(ctx->mu);
+    DeviceRestore dr;
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");   // types.go:20-22
     FileSet fs;
     RC_TRY(open_files(c, paths, n, fs));
-    if ((c->devs.size() > 1 || c->force_sharded) && n >= 2 * c->devs.size()) {
+    uint64_t bytes = 0, maxlen = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        bytes += fs.size[i];
+        maxlen = std::max(maxlen, fs.size[i]);
+    }
+    // 256 x 32 MiB segment files: one device (every chain resident; sharding only occupies more
+    // GPUs), so concurrent calls land on different devices
+    const int G = route_call(c, n, bytes, maxlen, DM_SRC_FILES);
+    if (sharded(c, G, n)) {
+        RangeLock lk(c, G);
         auto produce = [&](dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1) -> int {
             return files_leaves(cc, d, fs, l0, l1);
         };
-        return multi_root(c, n, produce, leaf_out, root);
+        return multi_root(c, G, n, produce, leaf_out, root);
     }
-    Dev& d = c->devs[0];
+    const int g = pick_device(c);
+    CallLock lk(c, g);
+    Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
     RC_TRY(files_leaves(c, d, fs, 0, n));
     return reduce_leaves_to_host(c, d, n, leaf_out, root);

@@ -359,7 +359,7 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
                        uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out, uint8_t fid[32]) {
     if (!r || !path || !savedir || !fid) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (nseg_out) *nseg_out = 0;
     FileSet fs;
     RC_TRY(open_files(c, &path, 1, fs));   // "open <path>: ..." first, as os.Open would fail

@@ -22,6 +22,8 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <memory>
 #include <future>
 #include <mutex>
 #include <string>
@@ -30,6 +32,7 @@
 
 #include "deoss_merkle.h"
 #include "merkle_kernels.hpp"
+#include "shard_plan.hpp"
 
 namespace {
 
@@ -114,14 +117,24 @@ struct Dev {
 
 }  // namespace
 
-struct dm_ctx {
+// Per-device call state of a context: the lock a call holds on the device it runs on, and the
+// device's load (calls running or waiting on it, plus open streams) for least-busy routing.
+struct DevSlot {
     std::mutex mu;
+    std::atomic<int> load{0};
+};
+
+struct dm_ctx {
     std::vector<Dev> devs;
-    std::vector<ncclComm_t> comms;
+    std::unique_ptr<DevSlot[]> slots;      // one per device (absent in private error-sink contexts)
+    std::atomic<uint32_t> rr{0};           // round-robin start of the least-busy scan
+    std::mutex comm_mu;
+    std::map<int, std::vector<ncclComm_t>> comms;   // RCCL communicators over devices [0, G'), by G'
+    std::mutex err_mu;
     std::string err;
-    bool timing = false;
-    int leaf_mode = DM_LEAF_AUTO;
-    // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-buffer objects through the
+    bool timing = false;                   // written with every device locked
+    std::atomic<int> leaf_mode{DM_LEAF_AUTO};
+    // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-memory objects through the
     // multi-device path (partition, RCCL all-gather, compaction, finish) even with one device.
     bool force_sharded = false;
 };
@@ -146,7 +159,10 @@ int fail(dm_ctx* c, int code, const char* fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
-    if (c) c->err = buf;
+    if (c) {
+        std::lock_guard<std::mutex> lk(c->err_mu);
+        c->err = buf;
+    }
     t_err = buf;
     return code;
 }
@@ -193,12 +209,81 @@ struct DeviceRestore {
     DeviceRestore& operator=(const DeviceRestore&) = delete;
 };
 
-// An entry point's hold on its context: the context lock, and the caller's device restored after.
+// An entry point's hold on ONE device of its context for the whole call (that device's scratch,
+// streams and staging), and the caller's device restored after.  Calls on different devices of one
+// context run concurrently; a thread holds at most one CallLock.
 struct CallLock {
     DeviceRestore dev;
-    std::lock_guard<std::mutex> lk;
-    explicit CallLock(std::mutex& m) : lk(m) {}
+    DevSlot* slot;
+    std::unique_lock<std::mutex> lk;
+    CallLock(dm_ctx* c, int g) : slot(&c->slots[g]) {
+        slot->load++;
+        lk = std::unique_lock<std::mutex>(slot->mu);
+    }
+    ~CallLock() {
+        lk.unlock();
+        slot->load--;
+    }
+    CallLock(const CallLock&) = delete;
+    CallLock& operator=(const CallLock&) = delete;
 };
+
+// Devices [0, G) of a context, locked in index order (so two of these cannot deadlock): sharded
+// calls (G = the devices they use) and context-wide settings (G = every device).
+struct RangeLock {
+    DeviceRestore dev;
+    dm_ctx* c;
+    int G;
+    std::vector<std::unique_lock<std::mutex>> lks;
+    RangeLock(dm_ctx* c_, int G_) : c(c_), G(G_) {
+        for (int g = 0; g < G; g++) c->slots[g].load++;
+        for (int g = 0; g < G; g++) lks.emplace_back(c->slots[g].mu);
+    }
+    explicit RangeLock(dm_ctx* c_) : RangeLock(c_, (int)c_->devs.size()) {}
+    ~RangeLock() {
+        for (auto& l : lks) l.unlock();
+        for (int g = 0; g < G; g++) c->slots[g].load--;
+    }
+    RangeLock(const RangeLock&) = delete;
+    RangeLock& operator=(const RangeLock&) = delete;
+};
+
+// Device for a call that can run anywhere: the least-loaded one, ties broken round-robin.
+int pick_device(dm_ctx* c) {
+    const int G = (int)c->devs.size();
+    if (G <= 1) return 0;
+    const int start = (int)(c->rr.fetch_add(1) % (uint32_t)G);
+    int best = start, best_load = c->slots[start].load.load();
+    for (int i = 1; i < G; i++) {
+        const int g = (start + i) % G;
+        const int l = c->slots[g].load.load();
+        if (l < best_load) {
+            best = g;
+            best_load = l;
+        }
+    }
+    return best;
+}
+
+// Calls already running or queued on the context (routing: a busy context never shards).
+int ctx_load(const dm_ctx* c) {
+    int s = 0;
+    for (size_t g = 0; g < c->devs.size(); g++) s += c->slots[g].load.load();
+    return s;
+}
+
+// Device holding device memory p (device-resident entry points run where their data lives);
+// the first device when p is not device memory of one of the context's devices.
+int device_of(dm_ctx* c, const void* p) {
+    if (c->devs.size() <= 1 || !p) return 0;
+    hipPointerAttribute_t attr{};
+    int g = 0;
+    if (hipPointerGetAttributes(&attr, p) == hipSuccess)
+        for (size_t i = 0; i < c->devs.size(); i++)
+            if (c->devs[i].id == attr.device) g = (int)i;
+    (void)hipGetLastError();
+    return g;
+}
 
 // Order this call's use of the context scratch after the previous call's (possibly other stream).
 int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
@@ -280,10 +365,8 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // 16,384 (536 vs 397 for K1P, 223 for K1Q in two rounds of workgroups); past that one lane per
 // leaf with >= 2 waves per SIMD wins.  K1P stays selectable (DM_LEAF_PAIR).
 int pick_leaf_kernel(const dm_ctx* c, const Dev& d, uint64_t n) {
-    if (c->leaf_mode != DM_LEAF_AUTO) return c->leaf_mode;
-    if (ceil_div(n, dm::kQuadLeaves) <= 4 * (uint64_t)d.cus) return DM_LEAF_QUAD;
-    if (ceil_div(n, dm::kLatLeaves) <= (uint64_t)d.cus) return DM_LEAF_LATENCY;
-    return DM_LEAF_WIDE;
+    static_assert(dm_plan::kQuadLeaves == dm::kQuadLeaves && dm_plan::kLatLeaves == dm::kLatLeaves, "plan shapes");
+    return dm_plan::leaf_kind(n, d.cus, c->leaf_mode.load());
 }
 
 template <bool TABLE, bool ALIGNED>
@@ -773,25 +856,34 @@ int reduce_leaves_to_host(dm_ctx* c, Dev& d, uint64_t n, uint8_t* leaf_out, uint
 // (stream-ordered on d.stream), reporting errors into its own context `cc`.
 using LeafProducer = std::function<int(dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1)>;
 
-// Multi-device single object: aligned leaf ranges per device (blocks of 2^k leaves, round-robin
-// free contiguous ranges), each device's leaf digests from ONE pass of `produce` (they feed both
-// the k-level subtree reduce and leaf_out), one RCCL all-gather of the 32-byte level-k nodes,
-// final levels on device 0.  Odd-node duplication only ever touches the global last node, which
-// lives in the last block, so the per-device nodes are exactly the global level-k nodes.
-int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf_out, uint8_t root[32]) {
-    const int G = (int)c->devs.size();
-    // block = 2^k leaves with at least 2 blocks per device when possible
-    uint32_t k = 0;
-    while (ceil_shift(n, k + 1) >= (uint64_t)(2 * G)) k++;
-    const uint64_t S = 1ull << k, nb = ceil_shift(n, k);
-    std::vector<uint64_t> b_lo(G), b_hi(G), cnt(G);
-    uint64_t maxc = 0;
-    for (int g = 0; g < G; g++) {
-        b_lo[g] = nb * g / G;
-        b_hi[g] = nb * (g + 1) / G;
-        cnt[g] = b_hi[g] - b_lo[g];
-        maxc = std::max(maxc, cnt[g]);
+// RCCL communicators over devices [0, G) of the context, created on first use (the caller holds
+// those devices' locks, so no other call is using them).
+int comms_for(dm_ctx* c, int G, std::vector<ncclComm_t>** out) {
+    std::lock_guard<std::mutex> lk(c->comm_mu);
+    auto it = c->comms.find(G);
+    if (it == c->comms.end()) {
+        std::vector<int> ids(G);
+        for (int g = 0; g < G; g++) ids[g] = c->devs[g].id;
+        std::vector<ncclComm_t> cm(G);
+        NCCL_TRY(ncclCommInitAll(cm.data(), G, ids.data()));
+        it = c->comms.emplace(G, std::move(cm)).first;
     }
+    *out = &it->second;
+    return DM_OK;
+}
+
+// Multi-device single object over devices [0, G) (the caller holds their locks): the aligned
+// partition of dm_plan::plan_shards (blocks of 2^k leaves, contiguous block ranges), each device's
+// leaf digests from ONE pass of `produce` (they feed both the k-level subtree reduce and
+// leaf_out), one RCCL all-gather of the 32-byte level-k nodes, final levels on device 0.  Odd-node
+// duplication only ever touches the global last node, which lives in the last block, so the
+// per-device nodes are exactly the global level-k nodes (shard_plan.hpp).
+int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_t* leaf_out, uint8_t root[32]) {
+    const dm_plan::Layout P = dm_plan::plan_shards(n, G);
+    const uint32_t k = P.k;
+    const uint64_t nb = P.nb, maxc = P.max_nodes();
+    std::vector<ncclComm_t>* comms = nullptr;
+    RC_TRY(comms_for(c, G, &comms));
     // order this call's scratch use after every call still queued on another stream of each device
     for (int g = 0; g < G; g++) RC_TRY(begin_call(c, c->devs[g], c->devs[g].stream));
     std::vector<int> rcs(G, DM_OK);
@@ -799,12 +891,12 @@ int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf
     auto work = [&](int g) {
         Dev& d = c->devs[g];
         dm_ctx local;   // private error sink (no devices: helpers given it must not index devs)
-        local.leaf_mode = c->leaf_mode;
+        local.leaf_mode = c->leaf_mode.load();
         dm_ctx* cc = &local;
         int rc = DM_OK;
         do {
             if (hipSetDevice(d.id) != hipSuccess) { rc = fail(cc, DM_ERR_HIP, "hipSetDevice(%d)", d.id); break; }
-            const uint64_t l0 = b_lo[g] * S, l1 = std::min(n, b_hi[g] * S);
+            const uint64_t l0 = P.leaf_lo(g), l1 = P.leaf_hi(g);
             if (d.gather.ensure(std::max<uint64_t>(maxc, 1) * 32 * (G + 1)) != hipSuccess) {
                 rc = fail(cc, DM_ERR_NOMEM, "gather slots");
                 break;
@@ -829,7 +921,9 @@ int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf
         rcs[g] = rc;
         errs[g] = local.err;
     };
-    {
+    if (G == 1) {
+        work(0);
+    } else {
         std::vector<std::thread> th;
         for (int g = 0; g < G; g++) th.emplace_back(work, g);
         for (auto& t : th) t.join();
@@ -845,7 +939,7 @@ int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf
     NCCL_TRY(ncclGroupStart());
     for (int g = 0; g < G; g++) {
         Dev& d = c->devs[g];
-        NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, c->comms[g], d.stream));
+        NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream));
     }
     NCCL_TRY(ncclGroupEnd());
     Dev& d0 = c->devs[0];
@@ -854,12 +948,10 @@ int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf
     // nodes_a/b) once device 0's leaf_out copy has left it
     HIP_TRY(hipStreamSynchronize(d0.stream));
     HIP_TRY(d0.leaves.ensure(std::max<uint64_t>(nb, 1) * 32 + 256));
-    uint64_t total = 0;
     for (int g = 0; g < G; g++) {
-        if (cnt[g] == 0) continue;
-        HIP_TRY(hipMemcpyAsync(d0.leaves.u8() + 32 * total, d0.gather.u8() + slot + g * slot, cnt[g] * 32,
-                               hipMemcpyDeviceToDevice, d0.stream));
-        total += cnt[g];
+        if (P.nodes(g) == 0) continue;
+        HIP_TRY(hipMemcpyAsync(d0.leaves.u8() + 32 * P.node_offset(g), d0.gather.u8() + slot + g * slot,
+                               P.nodes(g) * 32, hipMemcpyDeviceToDevice, d0.stream));
     }
     RC_TRY(finish(c, d0, d0.stream, d0.leaves.u8(), nb, k == 0, d0.root.u8()));
     HIP_TRY(hipMemcpyAsync(root, d0.root.p, 32, hipMemcpyDeviceToHost, d0.stream));
@@ -873,14 +965,109 @@ int multi_root(dm_ctx* c, uint64_t n, const LeafProducer& produce, uint8_t* leaf
 // Multi-device host buffer: each device stages its byte range through its own pinned ring (or
 // straight from pinned memory) with H2D overlapped with leaf hashing (h2d_and_hash_leaves:
 // stripes for few long leaves).
-int root_buffer_multi(dm_ctx* c, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out,
+int root_buffer_multi(dm_ctx* c, int G, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out,
                       uint8_t root[32]) {
     const uint64_t n = ceil_div(len, chunk);
     auto produce = [&](dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1) -> int {
         const uint64_t byte0 = l0 * chunk, byte1 = std::min(len, l1 * chunk);
         return h2d_and_hash_leaves(cc, d, static_cast<const uint8_t*>(host) + byte0, byte1 - byte0, chunk);
     };
-    return multi_root(c, n, produce, leaf_out, root);
+    return multi_root(c, G, n, produce, leaf_out, root);
+}
+
+// Source kind of host memory for routing: page-locked (crosses PCIe directly) or pageable.
+int host_src(const void* p) {
+    hipPointerAttribute_t attr{};
+    const bool pinned = p && hipPointerGetAttributes(&attr, p) == hipSuccess && attr.type == hipMemoryTypeHost;
+    (void)hipGetLastError();
+    return pinned ? DM_SRC_HOST_PINNED : DM_SRC_HOST_PAGEABLE;
+}
+
+// Devices a host-memory call uses (dm_plan::route; forced sharding is a test hook).
+int route_call(dm_ctx* c, uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, bool by_objects = false) {
+    const int G = (int)c->devs.size();
+    if (c->force_sharded) return n >= 2 * (uint64_t)G ? G : 1;
+    if (G <= 1) return 1;
+    return dm_plan::route(n, bytes, leaf_max, src, G, c->devs[0].cus, c->leaf_mode.load(), ctx_load(c), by_objects);
+}
+
+// Whether a call of n leaves routed to G devices takes the multi-device path (with
+// DEOSS_FORCE_SHARDED even G = 1 does, when n >= 2 x the context's devices).
+bool sharded(const dm_ctx* c, int G, uint64_t n) {
+    return G > 1 || (c->force_sharded && n >= 2 * (uint64_t)c->devs.size());
+}
+
+// Leaf digests of host chunks into d.leaves (stream-ordered on d.stream): read in place from
+// pinned memory by K1Q (zero-copy regime) or packed into HBM first.
+int chunks_leaves(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uint64_t n) {
+    std::vector<uint64_t> addr;
+    const bool zc = zero_copy_regime(c, d, n) && pinned_view(ptrs, lens, n, &addr);
+    if (!zc) RC_TRY(pack_chunks(c, d, ptrs, lens, n, addr));
+    bool aligned = true;
+    for (uint64_t i = 0; i < n && zc; i++) aligned &= addr[i] % 16 == 0;
+    RC_TRY(tables_begin(c, d, n * 16 + 1024));
+    HIP_TRY(d.leaves.ensure(n * 32));
+    RC_TRY(upload(c, d, d.stream, d.tab_addr, addr.data(), n * 8));
+    RC_TRY(upload(c, d, d.stream, d.tab_len, lens, n * 8));
+    dm::LeafArgs la{};
+    la.addrs = static_cast<const uint64_t*>(d.tab_addr.p);
+    la.lens = static_cast<const uint64_t*>(d.tab_len.p);
+    la.nleaves = n;
+    la.byte_end = ~0ull;
+    la.digests = d.leaves.u8();
+    return launch_leaves(c, d, d.stream, la, true, aligned, zc ? DM_LEAF_QUAD : pick_leaf_kernel(c, d, n));
+}
+
+// Host batch of objects on device d: roots (host, nobj x 32).
+int batch_host_on(dm_ctx* c, Dev& d, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
+                  uint8_t* roots) {
+    RC_TRY(begin_call(c, d, d.stream));
+    uint64_t T = 0;
+    for (uint64_t o = 0; o < nobj; o++) T += ceil_div(lens[o], chunk);
+    std::vector<uint64_t> addr;
+    const bool zc = zero_copy_regime(c, d, T) && pinned_view(objs, lens, nobj, &addr);
+    if (!zc) RC_TRY(pack_chunks(c, d, objs, lens, nobj, addr));
+    std::vector<const void*> dptr(nobj);
+    for (uint64_t o = 0; o < nobj; o++) dptr[o] = reinterpret_cast<const void*>(addr[o]);
+    HIP_TRY(d.gather.ensure(nobj * 32));
+    RC_TRY(batch_device(c, d, d.stream, dptr.data(), lens, nobj, chunk, d.gather.u8(), zc ? DM_LEAF_QUAD : -1));
+    HIP_TRY(hipMemcpyAsync(roots, d.gather.p, nobj * 32, hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    return DM_OK;
+}
+
+// Host batch over devices [0, G) (the caller holds their locks): device g takes a contiguous range
+// of objects with about 1/G of the leaves; objects never interact, so there is no exchange.
+int batch_host_multi(dm_ctx* c, int G, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
+                     uint8_t* roots) {
+    std::vector<uint64_t> first(nobj + 1, 0);
+    for (uint64_t o = 0; o < nobj; o++) first[o + 1] = first[o] + ceil_div(lens[o], chunk);
+    std::vector<uint64_t> o_lo(G + 1, nobj);
+    o_lo[0] = 0;
+    for (int g = 1; g < G; g++) {   // first object whose leaves start at or after g/G of the total
+        const uint64_t want = first[nobj] * (uint64_t)g / (uint64_t)G;
+        o_lo[g] = std::max<uint64_t>(o_lo[g - 1], (uint64_t)(std::lower_bound(first.begin(), first.end() - 1, want) - first.begin()));
+    }
+    std::vector<int> rcs(G, DM_OK);
+    std::vector<std::string> errs(G);
+    auto work = [&](int g) {
+        dm_ctx local;
+        local.leaf_mode = c->leaf_mode.load();
+        int rc = DM_OK;
+        const uint64_t a = o_lo[g], b = o_lo[g + 1];
+        if (b > a) {
+            if (hipSetDevice(c->devs[g].id) != hipSuccess) rc = fail(&local, DM_ERR_HIP, "hipSetDevice(%d)", c->devs[g].id);
+            else rc = batch_host_on(&local, c->devs[g], objs + a, lens + a, b - a, chunk, roots + 32 * a);
+        }
+        rcs[g] = rc;
+        errs[g] = local.err;
+    };
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++) th.emplace_back(work, g);
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; g++)
+        if (rcs[g] != DM_OK) return fail(c, rcs[g], "device %d: %s", c->devs[g].id, errs[g].c_str());
+    return DM_OK;
 }
 
 }  // namespace
@@ -948,6 +1135,7 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     }
     dm_ctx* c = new dm_ctx();
     c->devs.resize(ids.size());
+    c->slots.reset(new DevSlot[ids.size()]);
     for (size_t i = 0; i < ids.size(); i++) {
         c->devs[i].id = ids[i];
         int rc = init_device(c, c->devs[i]);
@@ -958,10 +1146,10 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     }
     const char* fs = std::getenv("DEOSS_FORCE_SHARDED");
     c->force_sharded = fs != nullptr && fs[0] == '1';
-    if (ids.size() > 1 || c->force_sharded) {
-        c->comms.resize(ids.size());
-        if (ncclCommInitAll(c->comms.data(), (int)ids.size(), ids.data()) != ncclSuccess) {
-            c->comms.clear();
+    if (ids.size() > 1 || c->force_sharded) {   // every device's communicator up front: fail here, not mid-call
+        std::vector<ncclComm_t>* cm = nullptr;
+        const int rc = comms_for(c, (int)ids.size(), &cm);
+        if (rc != DM_OK) {
             dm_destroy(c);
             return set_err(DM_ERR_RCCL, "ncclCommInitAll failed");
         }
@@ -973,27 +1161,27 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
 void dm_destroy(dm_ctx* ctx) {
     if (!ctx) return;
     DeviceRestore dev;
-    for (auto& cm : ctx->comms) (void)ncclCommDestroy(cm);
+    for (auto& kv : ctx->comms)
+        for (auto& cm : kv.second) (void)ncclCommDestroy(cm);
     for (auto& d : ctx->devs) destroy_device(d);
     delete ctx;
 }
 
 int dm_set_leaf_kernel(dm_ctx* ctx, int mode) {
     if (!ctx || mode < DM_LEAF_AUTO || mode > DM_LEAF_QUAD) return bad_arg();
-    CallLock lk(ctx->mu);
+    RangeLock lk(ctx);   // after every call in flight
     ctx->leaf_mode = mode;
     return DM_OK;
 }
 
 int dm_leaf_kernel_for(dm_ctx* ctx, uint64_t nleaves) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
     return pick_leaf_kernel(ctx, ctx->devs[0], nleaves);
 }
 
 int dm_set_timing(dm_ctx* ctx, int enable) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    RangeLock lk(ctx);
     ctx->timing = enable != 0;
     for (auto& d : ctx->devs) d.ntimed = 0;
     return DM_OK;
@@ -1001,7 +1189,7 @@ int dm_set_timing(dm_ctx* ctx, int enable) {
 
 int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double* total_ms_sum, double* leaf_ms_max) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    RangeLock lk(ctx);
     dm_ctx* c = ctx;
     uint64_t n = 0;
     double a = 0, b = 0, mx = 0;
@@ -1026,20 +1214,43 @@ int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double
     return DM_OK;
 }
 
+int dm_plan_shards(uint64_t nleaves, int ndev, uint32_t* levels, uint64_t* nblocks, uint64_t* leaf_lo,
+                   uint64_t* leaf_hi) {
+    if (ndev < 1 || !levels || !nblocks) return bad_arg();
+    const dm_plan::Layout P = dm_plan::plan_shards(nleaves, ndev);
+    *levels = P.k;
+    *nblocks = P.nb;
+    for (int g = 0; g < ndev; g++) {
+        if (leaf_lo) leaf_lo[g] = P.leaf_lo(g);
+        if (leaf_hi) leaf_hi[g] = P.leaf_hi(g);
+    }
+    return DM_OK;
+}
+
+int dm_plan_route(uint64_t nleaves, uint64_t bytes, uint64_t leaf_max, int source, int by_objects, int ndev, int cus,
+                  int leaf_mode, int busy, double* est_ms) {
+    if (ndev < 1 || cus < 1 || source < DM_SRC_DEVICE || source > DM_SRC_FILES || leaf_mode < DM_LEAF_AUTO ||
+        leaf_mode > DM_LEAF_QUAD)
+        return bad_arg();
+    return dm_plan::route(nleaves, bytes, leaf_max, source, ndev, cus, leaf_mode, busy, by_objects != 0, est_ms);
+}
+
 int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, void* dev_root,
                          void* leaf_out_dev, void* stream) {
     if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return bad_arg();
-    CallLock lk(ctx->mu);
-    Dev& d = ctx->devs[0];
+    const int g = device_of(ctx, dev);
+    CallLock lk(ctx, g);
+    Dev& d = ctx->devs[g];
     return root_device_impl(ctx, d, pick_stream(d, stream), dev, len, chunk, static_cast<uint8_t*>(dev_root),
                             static_cast<uint8_t*>(leaf_out_dev));
 }
 
 int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!dev && len)) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     RC_TRY(root_device_impl(c, d, d.stream, dev, len, chunk, d.root.u8(), nullptr));
     HIP_TRY(hipMemcpyAsync(root, d.root.p, 32, hipMemcpyDeviceToHost, d.stream));
     HIP_TRY(hipStreamSynchronize(d.stream));
@@ -1049,10 +1260,11 @@ int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, u
 int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint32_t levels,
                             void* dev_nodes, uint64_t* n_out, void* stream) {
     if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     dm::LeafArgs la = uniform_args(dev, len, chunk);
@@ -1066,10 +1278,11 @@ int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t
 int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int min_one_level, void* dev_root,
                            void* stream) {
     if (!ctx || !dev_nodes || !dev_root) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_nodes);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return finish(c, d, s, static_cast<const uint8_t*>(dev_nodes), n, min_one_level != 0,
@@ -1079,10 +1292,11 @@ int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int m
 int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const uint64_t* lens, uint64_t nobj,
                                uint64_t chunk, void* dev_roots, void* stream) {
     if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_roots);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return batch_device(c, d, s, dev_objs, lens, nobj, chunk, static_cast<uint8_t*>(dev_roots));
@@ -1090,10 +1304,11 @@ int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const u
 
 int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbytes, uint64_t seed, void* stream) {
     if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (nbytes == 0) return DM_OK;
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     const uint64_t nwords = nbytes / 8;
@@ -1108,9 +1323,10 @@ int dm_read_probe_async(dm_ctx* ctx, const void* dev, uint64_t nbytes, void* dev
     if (!ctx || !dev_xor8 || (!dev && nbytes) || nbytes % 16 || !is_aligned16(dev) ||
         reinterpret_cast<uintptr_t>(dev_xor8) % 8)
         return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_xor8);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     HIP_TRY(hipMemsetAsync(dev_xor8, 0, 8, s));
@@ -1127,70 +1343,76 @@ int dm_read_probe_async(dm_ctx* ctx, const void* dev, uint64_t nbytes, void* dev
 
 int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, uint8_t* leaf_out, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!host && len)) return bad_arg();
-    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
-    if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    if ((c->devs.size() > 1 || c->force_sharded) && ceil_div(len, chunk) >= 2 * c->devs.size())
-        return root_buffer_multi(c, host, len, chunk, leaf_out, root);
-    Dev& d = c->devs[0];
+    if (len == 0) {
+        DeviceRestore dr;
+        return fail(c, DM_ERR_EMPTY, "Empty data");
+    }
+    const uint64_t n = ceil_div(len, chunk);
+    const int G = route_call(c, n, len, std::min(len, chunk), host_src(host));
+    if (sharded(c, G, n)) {
+        RangeLock lk(c, G);
+        return root_buffer_multi(c, G, host, len, chunk, leaf_out, root);
+    }
+    const int g = pick_device(c);
+    CallLock lk(c, g);
+    Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
     RC_TRY(h2d_and_hash_leaves(c, d, host, len, chunk));
-    return reduce_leaves_to_host(c, d, ceil_div(len, chunk), leaf_out, root);
+    return reduce_leaves_to_host(c, d, n, leaf_out, root);
 }
 
 int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, uint64_t n, uint8_t* leaf_out,
                    uint8_t root[32]) {
     if (!ctx || !root || (n && (!ptrs || !lens))) return bad_arg();
-    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
+    DeviceRestore dr;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    for (uint64_t i = 0; i < n; i++)
+    uint64_t bytes = 0, maxlen = 0;
+    for (uint64_t i = 0; i < n; i++) {
         if (lens[i] && !ptrs[i]) return fail(c, DM_ERR_INVALID, "chunk %llu: NULL pointer", (unsigned long long)i);
-    Dev& d = c->devs[0];
+        bytes += lens[i];
+        maxlen = std::max(maxlen, lens[i]);
+    }
+    const int G = route_call(c, n, bytes, maxlen, host_src(ptrs[0]));
+    if (sharded(c, G, n)) {
+        RangeLock lk(c, G);
+        auto produce = [&](dm_ctx* cc, Dev& d, uint64_t l0, uint64_t l1) -> int {
+            return chunks_leaves(cc, d, ptrs + l0, lens + l0, l1 - l0);
+        };
+        return multi_root(c, G, n, produce, leaf_out, root);
+    }
+    const int g = pick_device(c);
+    CallLock lk(c, g);
+    Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
-    std::vector<uint64_t> addr;
-    const bool zc = zero_copy_regime(c, d, n) && pinned_view(ptrs, lens, n, &addr);
-    if (!zc) RC_TRY(pack_chunks(c, d, ptrs, lens, n, addr));
-    bool aligned = true;
-    for (uint64_t i = 0; i < n && zc; i++) aligned &= addr[i] % 16 == 0;
-    RC_TRY(tables_begin(c, d, n * 16 + 1024));
-    HIP_TRY(d.leaves.ensure(n * 32));
-    RC_TRY(upload(c, d, d.stream, d.tab_addr, addr.data(), n * 8));
-    RC_TRY(upload(c, d, d.stream, d.tab_len, lens, n * 8));
-    dm::LeafArgs la{};
-    la.addrs = static_cast<const uint64_t*>(d.tab_addr.p);
-    la.lens = static_cast<const uint64_t*>(d.tab_len.p);
-    la.nleaves = n;
-    la.byte_end = ~0ull;
-    la.digests = d.leaves.u8();
-    RC_TRY(launch_leaves(c, d, d.stream, la, true, aligned, zc ? DM_LEAF_QUAD : pick_leaf_kernel(c, d, n)));
+    RC_TRY(chunks_leaves(c, d, ptrs, lens, n));
     return reduce_leaves_to_host(c, d, n, leaf_out, root);
 }
 
 int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t chunk,
                   uint8_t* roots) {
     if (!ctx || chunk == 0 || (nobj && (!objs || !lens || !roots))) return bad_arg();
-    CallLock lk(ctx->mu);
     dm_ctx* c = ctx;
+    DeviceRestore dr;
     if (nobj == 0) return DM_OK;
+    uint64_t T = 0, bytes = 0, maxlen = 0;
     for (uint64_t o = 0; o < nobj; o++) {
         if (lens[o] == 0) return fail(c, DM_ERR_EMPTY, "Empty data (object %llu has no bytes)", (unsigned long long)o);
         if (!objs[o]) return fail(c, DM_ERR_INVALID, "object %llu: NULL pointer", (unsigned long long)o);
+        T += ceil_div(lens[o], chunk);
+        bytes += lens[o];
+        maxlen = std::max(maxlen, std::min(lens[o], chunk));
     }
-    Dev& d = c->devs[0];
-    RC_TRY(begin_call(c, d, d.stream));
-    uint64_t T = 0;
-    for (uint64_t o = 0; o < nobj; o++) T += ceil_div(lens[o], chunk);
-    std::vector<uint64_t> addr;
-    const bool zc = zero_copy_regime(c, d, T) && pinned_view(objs, lens, nobj, &addr);
-    if (!zc) RC_TRY(pack_chunks(c, d, objs, lens, nobj, addr));
-    std::vector<const void*> dptr(nobj);
-    for (uint64_t o = 0; o < nobj; o++) dptr[o] = reinterpret_cast<const void*>(addr[o]);
-    HIP_TRY(d.gather.ensure(nobj * 32));
-    RC_TRY(batch_device(c, d, d.stream, dptr.data(), lens, nobj, chunk, d.gather.u8(), zc ? DM_LEAF_QUAD : -1));
-    HIP_TRY(hipMemcpyAsync(roots, d.gather.p, nobj * 32, hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    return DM_OK;
+    // objects are independent: several devices take contiguous object ranges, no exchange
+    const int G = std::min<uint64_t>(route_call(c, T, bytes, maxlen, host_src(objs[0]), true), nobj);
+    if (G > 1) {
+        RangeLock lk(c, G);
+        return batch_host_multi(c, G, objs, lens, nobj, chunk, roots);
+    }
+    const int g = pick_device(c);
+    CallLock lk(c, g);
+    return batch_host_on(c, c->devs[g], objs, lens, nobj, chunk, roots);
 }
 
 }  // extern "C"

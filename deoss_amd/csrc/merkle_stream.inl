@@ -156,6 +156,7 @@ int stream_flush(dm_stream* st) {
 
 void stream_free(dm_stream* st) {
     if (!st) return;
+    st->c->slots[st->dev].load--;   // the stream's hold on its device's load (dm_stream_open)
     (void)hipSetDevice(st->c->devs[st->dev].id);
     if (st->copy) (void)hipStreamSynchronize(st->copy);
     for (int k = 0; k < kStreamLanes; k++)
@@ -192,18 +193,19 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     if (!ctx || !out || chunk == 0) return bad_arg();
     *out = nullptr;
     DeviceRestore dev;
-    if (chunk % 16 != 0) {
-        CallLock lk(ctx->mu);
-        return fail(ctx, DM_ERR_INVALID, "dm_stream: chunk must be a multiple of 16 bytes");
-    }
+    if (chunk % 16 != 0) return fail(ctx, DM_ERR_INVALID, "dm_stream: chunk must be a multiple of 16 bytes");
     dm_stream* st = new dm_stream();
     st->c = ctx;
+    // a stream keeps one device busy while the body arrives: the least-loaded one, counted in its
+    // load until the stream is freed, so concurrent uploads spread over the context's devices
+    st->dev = pick_device(ctx);
+    ctx->slots[st->dev].load++;
     st->chunk = chunk;
     st->seg_leaves = std::max<uint64_t>(1, (1ull << 30) / chunk);
     int rc = DM_OK;
     do {
         hipError_t e;
-        if ((e = hipSetDevice(ctx->devs[0].id)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "hipSetDevice", e); break; }
+        if ((e = hipSetDevice(ctx->devs[st->dev].id)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "hipSetDevice", e); break; }
         // copies on a high-priority stream (its own hardware queue): staging reuse must not wait
         // behind long leaf kernels
         int lo = 0, hi = 0;
@@ -227,8 +229,10 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
         }
     } while (0);
     if (rc != DM_OK) {
-        CallLock lk(ctx->mu);
-        ctx->err = st->err;
+        {
+            std::lock_guard<std::mutex> lk(ctx->err_mu);
+            ctx->err = st->err;
+        }
         t_err = st->err;
         stream_free(st);
         return rc;
@@ -314,7 +318,7 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         if ((rc = stream_launch(st, n, st->received - (n - 1) * st->chunk)) != DM_OK) break;
         if (nleaves) *nleaves = n;
         // tree over all leaf digests on the context's stream, after every compute stream
-        CallLock lk(c->mu);
+        CallLock lk(c, st->dev);
         Dev& d = c->devs[st->dev];
         hipStream_t s = d.stream;
         if ((rc = begin_call(c, d, s)) != DM_OK) break;
@@ -342,7 +346,7 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         if ((e = hipStreamSynchronize(s)) != hipSuccess) rc = fail(c, DM_ERR_HIP, "close sync: %s", hipGetErrorString(e));
     } while (0);
     if (rc != DM_OK && !st->err.empty()) {
-        CallLock lk(c->mu);
+        std::lock_guard<std::mutex> lk(c->err_mu);
         if (c->err.empty() || rc == DM_ERR_EMPTY) c->err = st->err;
         if (t_err.empty() || rc == DM_ERR_EMPTY) t_err = st->err;
     }

@@ -151,7 +151,7 @@ int dm_process_device_async(dm_rs* r, void* dev_obj, uint64_t len, uint64_t segm
                             void* dev_seg_hashes, void* dev_frag_hashes, void* dev_fid, void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     RC_TRY(process_check(r, len, segment));
     if (!dev_obj || !dev_parity || !dev_fid || !is_aligned16(dev_obj) || !is_aligned16(dev_parity))
         return fail(c, DM_ERR_INVALID, "dm_process_device_async: need 16-byte aligned object and parity buffers");
@@ -165,7 +165,7 @@ int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment
                       uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t fid[32]) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (!fid || (!host && len)) return fail(c, DM_ERR_INVALID, "dm_process_buffer: null argument");
     RC_TRY(process_check(r, len, segment));
     return process_host(r, c->devs[0], &host, &len, 1, segment, &frags_out, &seg_hashes, &frag_hashes, fid);
@@ -175,7 +175,7 @@ int dm_process_batch(dm_rs* r, const void* const* objs, const uint64_t* lens, ui
                      void* const* frags_out, uint8_t* const* seg_hashes, uint8_t* const* frag_hashes, uint8_t* fids) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (nobj == 0) return DM_OK;
     if (!objs || !lens || !fids) return fail(c, DM_ERR_INVALID, "dm_process_batch: null argument");
     for (uint64_t o = 0; o < nobj; o++) {

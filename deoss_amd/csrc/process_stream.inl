@@ -297,7 +297,7 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
     *out = nullptr;
     dm_ctx* c = r->c;
     {
-        CallLock lk(c->mu);
+        CallLock lk(c, 0);
         RC_TRY(process_check(r, 1, segment));
     }
     DeviceRestore dev;
@@ -446,7 +446,7 @@ int pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uin
         }
         if (rc != DM_OK) break;
         {   // fid: the tree over every segment digest, on the context
-            CallLock lk(c->mu);
+            CallLock lk(c, 0);
             Dev& d = ps_dev(st);
             hipStream_t s = d.stream;
             if ((rc = begin_call(c, d, s)) != DM_OK) break;

@@ -174,7 +174,7 @@ extern "C" {
 int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
     if (!ctx || !out) return bad_arg();
     *out = nullptr;
-    CallLock lk(ctx->mu);
+    CallLock lk(ctx, 0);
     dm_ctx* c = ctx;
     if (data_shards < 1 || data_shards > dm::kRsMaxIn || parity_shards < 1 || parity_shards > dm::kRsMaxOut)
         return fail(c, DM_ERR_INVALID, "shard counts: 1 <= data <= %d, 1 <= parity <= %d", dm::kRsMaxIn,
@@ -219,7 +219,7 @@ int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
 void dm_rs_destroy(dm_rs* r) {
     if (!r) return;
     {
-        CallLock lk(r->c->mu);
+        CallLock lk(r->c, 0);
         (void)hipSetDevice(r->c->devs[0].id);
         (void)hipDeviceSynchronize();
         r->enc_tab.release();
@@ -240,7 +240,7 @@ int dm_rs_encode_device_async(dm_rs* r, const void* data, uint64_t data_stride, 
                               uint64_t shard, uint64_t nseg, void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (!data || !parity || nseg == 0 || shard == 0 || shard % 16 || data_stride % 16 || parity_stride % 16 ||
         !is_aligned16(data) || !is_aligned16(parity))
         return fail(c, DM_ERR_INVALID, "dm_rs_encode_device_async: need 16-byte aligned shards, strides and sizes");
@@ -271,7 +271,7 @@ int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t*
                                    void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (!shards || !present || shard == 0 || shard % 16)
         return fail(c, DM_ERR_INVALID, "dm_rs_reconstruct_device_async: shard bytes must be a multiple of 16");
     for (int i = 0; i < r->k + r->m; i++)
@@ -288,7 +288,7 @@ int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t*
 int dm_rs_encode(dm_rs* r, const void* const* data, void* const* parity, uint64_t shard) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     if (!data || !parity || shard == 0) return fail(c, DM_ERR_INVALID, "dm_rs_encode: null shards or zero size");
     for (int j = 0; j < r->k; j++)
         if (!data[j]) return fail(c, DM_ERR_INVALID, "dm_rs_encode: data shard %d is null", j);
@@ -338,7 +338,7 @@ int dm_rs_encode_buffer(dm_rs* r, const void* host, uint64_t len, void* out, uin
 int dm_rs_reconstruct(dm_rs* r, void* const* shards, const uint8_t* present, uint64_t shard) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c->mu);
+    CallLock lk(c, 0);
     const int total = r->k + r->m;
     if (!shards || !present || shard == 0) return fail(c, DM_ERR_INVALID, "dm_rs_reconstruct: bad arguments");
     for (int i = 0; i < total; i++)

@@ -116,12 +116,13 @@ uint32_t dm_tree_depth(uint64_t n) { return tree_depth(n); }
 
 int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n, void* dev_nodes, void* stream) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_nodes);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (!aligned_all({dev_leaves, dev_nodes}))
         return fail(c, DM_ERR_INVALID, "dm_tree_levels_device_async: need 16-byte aligned device buffers");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return tree_levels_dev(c, s, static_cast<const uint8_t*>(dev_leaves), n, static_cast<uint8_t*>(dev_nodes));
@@ -129,10 +130,11 @@ int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n,
 
 int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t* nodes_out) {
     if (!ctx || (n && (!leaf_digests || !nodes_out))) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = pick_device(ctx);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = d.stream;
     RC_TRY(begin_call(c, d, s));
     const uint64_t T = tree_nodes(n);
@@ -148,14 +150,15 @@ int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t
 int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void* dev_nodes, uint64_t n,
                                  const void* dev_idx, uint64_t q, void* dev_paths, void* dev_bits, void* stream) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_paths);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
     if (!aligned_all({dev_leaves, dev_nodes, dev_paths}) || !dev_idx || !dev_bits ||
         (reinterpret_cast<uintptr_t>(dev_idx) & 7))
         return fail(c, DM_ERR_INVALID, "dm_merkle_paths_device_async: null or misaligned device buffer");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return paths_dev(c, s, static_cast<const uint8_t*>(dev_leaves), static_cast<const uint8_t*>(dev_nodes), n,
@@ -166,11 +169,12 @@ int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void
 int dm_merkle_paths(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, const uint64_t* idx, uint64_t q,
                     uint8_t* paths, uint8_t* bits) {
     if (!ctx || (n && !leaf_digests) || (q && (!idx || !paths || !bits))) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = pick_device(ctx);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = d.stream;
     RC_TRY(begin_call(c, d, s));
     const uint64_t T = tree_nodes(n);
@@ -195,7 +199,8 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
                                  const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                  uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_ok);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     if (!dev_contents || !lens || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
@@ -204,7 +209,7 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
     for (uint64_t t = 0; t < q; t++)
         if (lens[t] && !dev_contents[t])
             return fail(c, DM_ERR_INVALID, "content %llu: NULL pointer", (unsigned long long)t);
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return verify_dev(c, d, s, dev_contents, lens, q, static_cast<const uint8_t*>(dev_paths),
@@ -216,13 +221,14 @@ int dm_verify_object_device_async(dm_ctx* ctx, const void* dev_obj, uint64_t len
                                   const void* dev_paths, const void* dev_bits, uint32_t depth, const void* dev_roots,
                                   uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = device_of(ctx, dev_obj);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (chunk == 0 || !dev_obj || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
         root_stride % 16)
         return fail(c, DM_ERR_INVALID, "dm_verify_object_device_async: null or misaligned argument, or depth 0");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return verify_object_dev(c, d, s, dev_obj, len, chunk, static_cast<const uint8_t*>(dev_paths),
@@ -235,12 +241,13 @@ int dm_verify_paths(dm_ctx* ctx, const void* const* contents, const uint64_t* le
     if (!ctx || (q && (!contents || !lens || !paths || !bits || !roots || !ok)) || depth == 0 ||
         (root_stride != 0 && root_stride != 32))
         return bad_arg();
-    CallLock lk(ctx->mu);
+    const int g = pick_device(ctx);
+    CallLock lk(ctx, g);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     for (uint64_t t = 0; t < q; t++)
         if (lens[t] && !contents[t]) return fail(c, DM_ERR_INVALID, "content %llu: NULL pointer", (unsigned long long)t);
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = d.stream;
     RC_TRY(begin_call(c, d, s));
     std::vector<uint64_t> addr;

@@ -49,20 +49,25 @@ class ShardPlan:
 
 
 def plan_shards(length: int, chunk: int, world: int) -> ShardPlan:
-    """Pick k: the largest block that still gives every rank an equal share when n divides
-    evenly, otherwise at least two blocks per rank (load balance within one block)."""
+    """The library's partition rule (deoss_amd/csrc/shard_plan.hpp dm_plan::plan_shards, exported as
+    dm_plan_shards; tests/test_dispatch_plan.py checks both agree): k = the largest block size that
+    keeps every rank within 1/8 of an even split of the leaves and gives every rank at least one
+    block (k = 0 when n < world), never more than ceil(log2 n) levels."""
     if length <= 0 or chunk <= 0 or world <= 0:
         raise ValueError("length, chunk and world must be positive")
     n = (length + chunk - 1) // chunk
+    even = (n + world - 1) // world
     best = 0
-    for k in range(0, 63):
+    k = 0
+    while k < 63 and (k == 0 or (1 << (k - 1)) < n):
         nb = _ceil_shift(n, k)
         if nb < world:
             break
-        if n % (world << k) == 0 or nb >= 2 * world:
+        plan = ShardPlan(length=length, chunk=chunk, world=world, k=k, n_leaves=n, n_blocks=nb)
+        if 8 * max(l1 - l0 for l0, l1 in (plan.leaf_range(r) for r in range(world))) <= 9 * even:
             best = k
-    nb = _ceil_shift(n, best)
-    return ShardPlan(length=length, chunk=chunk, world=world, k=best, n_leaves=n, n_blocks=nb)
+        k += 1
+    return ShardPlan(length=length, chunk=chunk, world=world, k=best, n_leaves=n, n_blocks=_ceil_shift(n, best))
 
 
 def parity_prefix(length: int, chunk: int, cap_bytes: int) -> int:

@@ -17,7 +17,12 @@
  *    n x 32 bytes in chunk order (leaf_out may be NULL).  merkletree's duplicated last leaf
  *    for odd n is NOT written (it equals leaf n-1).
  *  - Ownership: the caller owns every buffer; nothing is retained after return.
- *  - Threading: a context serialises its calls internally; separate contexts run in parallel.
+ *  - Threading: every call holds ONE device of its context (a per-device lock) for its duration;
+ *    calls on different devices of one context run in parallel, calls on one device queue.  Host-
+ *    memory calls (dm_root_buffer / _chunks / _batch, dm_new_hash_tree, streams) go to the least-
+ *    loaded device, or are sharded over several devices when dm_plan_route says that finishes
+ *    sooner (never while other calls are in flight); device-memory calls run on the device that
+ *    holds their memory; an rs (dm_rs_*, FullProcessing) lives on its context's first device.
  *  - Every call leaves the calling thread's current HIP device as it found it (the library
  *    switches to its context's devices inside the call and switches back).
  *  - `stream` arguments are hipStream_t values passed as void*, used verbatim (NULL is HIP's
@@ -52,8 +57,10 @@ enum {
 };
 
 /* Context over one or more GPUs of this process.  devs == NULL/ndev <= 0: device 0 only.
- * With ndev > 1 the host-buffer entry points shard a single object by aligned chunk ranges
- * across the devices and gather per-device subtree roots with RCCL (DESIGN.md "C1"). */
+ * With ndev > 1, each host-memory call runs whole on the least-loaded device, unless dm_plan_route
+ * shards it: a single object is then split by aligned chunk ranges across devices [0, G') and the
+ * per-device subtree roots are gathered with RCCL ("C1"); a batch is split by
+ * objects with no exchange. */
 int dm_create(dm_ctx **out, const int *devs, int ndev);
 void dm_destroy(dm_ctx *ctx);
 const char *dm_strerror(int rc);
@@ -304,6 +311,23 @@ int dm_batcher_process(dm_batcher *b, const void *host, uint64_t len, void *frag
 int dm_batcher_stats(dm_batcher *b, uint64_t *requests, uint64_t *batches, uint64_t *max_batch);
 /* Message of the calling thread's last failing dm_batcher_* call. */
 const char *dm_batcher_last_error(void);
+
+/* ---- multi-device plan (pure host functions: no GPU, no context) ---------------------------
+ * The partition and routing rules the library applies (deoss_amd/csrc/shard_plan.hpp), exported so
+ * the one-process-per-GPU path (deoss_amd/sharding.py) and the tests use the same rule. */
+enum { DM_SRC_DEVICE = 0, DM_SRC_HOST_PINNED = 1, DM_SRC_HOST_PAGEABLE = 2, DM_SRC_FILES = 3 };
+/* Partition of nleaves leaves over ndev devices: blocks of 2^levels leaves (*levels), *nblocks
+ * blocks (= the level-`levels` nodes of the global tree), device g owns leaves [leaf_lo[g],
+ * leaf_hi[g]) (arrays of ndev entries, nullable). */
+int dm_plan_shards(uint64_t nleaves, int ndev, uint32_t *levels, uint64_t *nblocks, uint64_t *leaf_lo,
+                   uint64_t *leaf_hi);
+/* Devices a call should use (1 = whole call on one device) for nleaves leaves, `bytes` in total,
+ * the longest leaf leaf_max bytes, starting at `source` (DM_SRC_*), split by objects (by_objects != 0,
+ * a batch) or as one tree, with ndev devices of `cus` compute units, leaf-kernel mode leaf_mode
+ * (DM_LEAF_*) and `busy` calls already in flight.  est_ms (nullable, ndev entries): the cost
+ * model's time for 1 .. ndev devices. */
+int dm_plan_route(uint64_t nleaves, uint64_t bytes, uint64_t leaf_max, int source, int by_objects, int ndev, int cus,
+                  int leaf_mode, int busy, double *est_ms);
 
 /* ---- tuning ------------------------------------------------------------------------------ */
 

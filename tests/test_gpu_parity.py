@@ -425,6 +425,13 @@ def test_single_process_sharded_path(oracle_lib):
             assert root == want, (length, chunk)
             assert leaves == lw, (length, chunk)
             assert bytes(r.cpu().numpy()) == want_other, (length, chunk)
+        # dm_root_chunks through the same partition (chunk lists: ragged, empty chunks, odd n)
+        for n, base in [(600, 3000), (2, 70000), (257, 64), (1000, 1)]:
+            chunks = [oracle_lib.splitmix_bytes((base * (i % 7)) % 100003, 900 + i) for i in range(n)]
+            lw, want = oracle_lib.root_chunks(chunks, nthreads=8)
+            leaves, root = c.root_chunks(chunks)
+            assert root == want, n
+            assert leaves == lw, n
     finally:
         c.close()
 
