@@ -32,7 +32,29 @@ def up_to_date(out: str = OUT) -> bool:
     return all(os.path.getmtime(p) <= t for p in [SRC, *HDRS])
 
 
+PC = os.path.join(HERE, "deoss_merkle.pc")
+
+
+def write_pkg_config(path: str = PC) -> str:
+    """deoss_merkle.pc for the Go bindings' `#cgo pkg-config: deoss_merkle`: the
+    include and library directories of THIS checkout, so the go/ packages resolve the library
+    wherever they are copied (PKG_CONFIG_PATH=<checkout>/deoss_amd)."""
+    text = (f"prefix={ROOT}\n"
+            "includedir=${prefix}/include\n"
+            "libdir=${prefix}/deoss_amd\n\n"
+            "Name: deoss_merkle\n"
+            "Description: MI355X-native Merkle content hashing for DeOSS (C ABI include/deoss_merkle.h)\n"
+            "Version: 0.3.0\n"
+            "Cflags: -I${includedir}\n"
+            "Libs: -L${libdir} -ldeoss_merkle -Wl,-rpath,${libdir}\n")
+    if not os.path.exists(path) or open(path).read() != text:
+        with open(path, "w") as f:
+            f.write(text)
+    return path
+
+
 def build(force: bool = False, verbose: bool = True) -> str:
+    write_pkg_config()
     if not force and up_to_date():
         return OUT
     cmd = hipcc_cmd()

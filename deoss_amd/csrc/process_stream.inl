@@ -14,6 +14,11 @@
 //     batches arrive);
 //   - close pads the last segment, launches the last chunk and batch, drains the parity, builds
 //     the fid over all segment digests and renames every temporary to savedir/<hex SHA-256>.
+// Device memory is bounded, not proportional to the body: a chunk's buffer (3 x its segments at
+// 4 + 8) returns to the stream's spare list once its parity has been written out and the leaf
+// launch that hashed it has finished, and new chunks reuse spare buffers.  When the buffers held
+// reach the cap (DEOSS_PS_DEVICE_CAP, default kPsDeviceCap), write blocks: it launches the pending
+// batch early and waits for the oldest chunk to be reclaimable.
 // Results are those of dm_full_processing on the same bytes.  Part of merkle_capi.hip (after
 // fullproc_capi.inl: SlotWrites, write_whole, mkdir_all, hex32, env_bytes).
 
@@ -22,12 +27,18 @@ namespace {
 constexpr int kPsSlots = 4;
 constexpr uint64_t kPsSlotBytes = 64ull << 20;
 constexpr uint64_t kPsBatchChunks = 32;   // 64 segments = 2 GiB of body per leaf launch (32 MiB segments)
+// Device bytes one pstream may hold: two 6 GiB batches in flight (32 chunks x 2 segments x 96 MiB)
+// plus the chunks arriving meanwhile, so both leaf lanes stay busy at full rate.
+constexpr uint64_t kPsDeviceCap = 16ull << 30;
+
+struct PsBatch;
 
 struct PsChunk {
     uint64_t s0 = 0, ns = 0;      // segments [s0, s0 + ns)
     DevBuf mem;                   // ns * seg of data, then ns * pbytes of parity
     hipEvent_t ev_rs = nullptr;   // RS done: parity may be copied out
-    bool drained = false;
+    bool drained = false;         // parity written out (its D2H has completed)
+    PsBatch* batch = nullptr;     // the leaf launch that hashes this chunk (nullptr: not launched yet)
 };
 
 struct PsBatch {
@@ -35,6 +46,7 @@ struct PsBatch {
     DevBuf tab, dig;                            // leaf table; digests: ns segments, then ns x total fragments
     PinnedBuf htab;
     int lane = 0;
+    hipEvent_t ev_done = nullptr;               // the leaf launch has finished reading its chunks
 };
 
 }  // namespace
@@ -58,6 +70,9 @@ struct dm_pstream {
     std::vector<PsBatch*> batches;
     uint64_t hashed_chunks = 0;     // chunks covered by leaf launches
     uint64_t drained_upto = 0;      // chunks [0, drained_upto) have their parity written
+    uint64_t reclaimed_upto = 0;    // chunks [0, reclaimed_upto) gave their device buffer back
+    std::vector<DevBuf> spare;      // reclaimed chunk buffers, reused by later chunks
+    uint64_t dev_cap = kPsDeviceCap, dev_held = 0, dev_peak = 0;   // chunk buffers allocated (in use + spare)
     std::vector<std::pair<std::string, uint64_t>> pend;   // temporary, digest index (~: segment)
     std::string err;
     int failed = DM_OK;   // sticky: after a failed write the stream only aborts (close returns this)
@@ -193,8 +208,69 @@ int ps_launch_batch(dm_pstream* st, uint64_t upto) {
     la.digests = b->dig.u8();
     launch_leaves_t<true, true>(s, la, pick_leaf_kernel(st->r->c, d, T), d.cus);
     PSHIP(hipGetLastError());
+    PSHIP(hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
+    PSHIP(hipEventRecord(b->ev_done, s));
+    for (uint64_t c = b->c0; c < upto; c++) st->chunks[c]->batch = b;
     st->hashed_chunks = upto;
     return DM_OK;
+}
+
+// Return the buffers of chunks whose parity is written out and whose leaf launch has finished to
+// the spare list, oldest first (drains and launches run in chunk order).  wait: block for the
+// oldest chunk that is still in use (after launching its batch and draining its parity).
+int ps_reclaim(dm_pstream* st, bool wait) {
+    while (st->reclaimed_upto < st->chunks.size()) {
+        PsChunk* ch = st->chunks[st->reclaimed_upto];
+        if (wait && !ch->batch) RC_TRY(ps_launch_batch(st, st->chunks.size()));
+        if (wait && !ch->drained) RC_TRY(ps_drain(st, true));
+        if (!ch->batch || !ch->drained) break;
+        if (wait) {
+            PSHIP(hipEventSynchronize(ch->batch->ev_done));
+        } else {
+            const hipError_t q = hipEventQuery(ch->batch->ev_done);
+            if (q == hipErrorNotReady) break;
+            PSHIP(q);
+        }
+        st->spare.push_back(ch->mem);
+        ch->mem = DevBuf();
+        st->reclaimed_upto++;
+        wait = false;   // one chunk freed is enough to make progress
+    }
+    return DM_OK;
+}
+
+// A device buffer of `bytes` for the next chunk: a spare one, a new one within the cap, or (cap
+// reached) the oldest in-use buffer once it can be reclaimed.
+int ps_chunk_buffer(dm_pstream* st, uint64_t bytes, DevBuf* out) {
+    RC_TRY(ps_reclaim(st, false));
+    for (;;) {
+        for (size_t i = 0; i < st->spare.size(); i++)
+            if (st->spare[i].cap >= bytes) {
+                *out = st->spare[i];
+                st->spare.erase(st->spare.begin() + (ptrdiff_t)i);
+                return DM_OK;
+            }
+        const uint64_t sz = round_up(std::max<uint64_t>(bytes, 4096), 2ull << 20);
+        if (st->dev_held + sz <= st->dev_cap || st->reclaimed_upto == st->chunks.size()) {
+            DevBuf b;
+            PSHIP(b.ensure(sz));
+            st->dev_held += b.cap;
+            st->dev_peak = std::max(st->dev_peak, st->dev_held);
+            *out = b;
+            return DM_OK;
+        }
+        if (!st->spare.empty()) {   // spare buffers too small for this chunk: give them back first
+            for (auto& b : st->spare) {
+                st->dev_held -= b.cap;
+                b.release();
+            }
+            st->spare.clear();
+            continue;
+        }
+        const uint64_t before = st->reclaimed_upto;
+        RC_TRY(ps_reclaim(st, true));
+        if (st->reclaimed_upto == before) return pfail(st, DM_ERR_NOMEM, "pstream: device cap reached, nothing to reclaim");
+    }
 }
 
 // The current slot holds `len` bytes (whole segments, the last one zero-padded at close): copy it
@@ -211,7 +287,7 @@ int ps_flush(dm_pstream* st) {
     ch->s0 = st->chunks.size() > 1 ? st->chunks[st->chunks.size() - 2]->s0 + st->chunks[st->chunks.size() - 2]->ns : 0;
     ch->ns = ns;
     PSHIP(hipEventCreateWithFlags(&ch->ev_rs, hipEventDisableTiming));
-    PSHIP(ch->mem.ensure(ns * (st->seg + st->pbytes)));
+    RC_TRY(ps_chunk_buffer(st, ns * (st->seg + st->pbytes), &ch->mem));
     PSHIP(hipMemcpyAsync(ch->mem.p, buf, len, hipMemcpyHostToDevice, st->copy));
     PSHIP(hipEventRecord(st->ev_slot[sl], st->copy));
     std::vector<FpFile> files;
@@ -263,10 +339,12 @@ void ps_free(dm_pstream* st) {
         if (ch->ev_rs) (void)hipEventDestroy(ch->ev_rs);
         delete ch;
     }
+    for (auto& b : st->spare) b.release();
     for (PsBatch* b : st->batches) {
         b->tab.release();
         b->dig.release();
         b->htab.release();
+        if (b->ev_done) (void)hipEventDestroy(b->ev_done);
         delete b;
     }
     for (auto& b : st->slot) b.release();
@@ -313,6 +391,7 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
     // test hooks (env, read at open): small slots / batches exercise slot reuse and many launches
     const uint64_t slot_bytes = env_bytes("DEOSS_FP_SLOT_BYTES", kPsSlotBytes);
     st->batch_chunks = env_bytes("DEOSS_PS_BATCH_CHUNKS", kPsBatchChunks);
+    st->dev_cap = env_bytes("DEOSS_PS_DEVICE_CAP", kPsDeviceCap);
     st->spd = std::max<uint64_t>(1, slot_bytes / segment);
     st->spp = std::max<uint64_t>(1, slot_bytes / st->pbytes);
     st->slot_len = st->spd * segment;
@@ -489,6 +568,13 @@ int pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uin
 }  // namespace
 
 extern "C" {
+
+int dm_pstream_stats(dm_pstream* st, uint64_t* device_bytes, uint64_t* peak_device_bytes) {
+    if (!st) return bad_arg();
+    if (device_bytes) *device_bytes = st->dev_held;
+    if (peak_device_bytes) *peak_device_bytes = st->dev_peak;
+    return DM_OK;
+}
 
 void dm_pstream_abort(dm_pstream* st) {
     if (!st) return;

@@ -245,6 +245,7 @@ class ProcessingStream:
         self._L = proc.ctx._L
         self.savedir = savedir
         self.written = 0
+        self.device_bytes = self.peak_device_bytes = 0
         h = ctypes.c_void_p()
         if segment_files is None:
             segment_files = _write_segments()
@@ -293,6 +294,7 @@ class ProcessingStream:
         frag = ctypes.create_string_buffer(32 * cap * total)
         fid = ctypes.create_string_buffer(32)
         nseg = ctypes.c_uint64(0)
+        self.device_bytes, self.peak_device_bytes = self.stats()
         h, self._h = self._h, None
         self._raise(self._L.dm_pstream_close(h, seg, frag, cap, ctypes.byref(nseg), fid), "dm_pstream_close")
         n = nseg.value
@@ -304,6 +306,15 @@ class ProcessingStream:
         self.segment_digests = seg.raw[:32 * n]
         self.fragment_digests = frag.raw[:32 * n * total]
         return info, fid.raw.hex()
+
+    def stats(self) -> Tuple[int, int]:
+        """(device bytes the stream holds now, the most it has held): chunk buffers in use or spare,
+        bounded by DEOSS_PS_DEVICE_CAP (default 16 GiB), not by the body size."""
+        if self._h is None:
+            return self.device_bytes, self.peak_device_bytes
+        cur, peak = ctypes.c_uint64(), ctypes.c_uint64()
+        self._raise(self._L.dm_pstream_stats(self._h, ctypes.byref(cur), ctypes.byref(peak)), "dm_pstream_stats")
+        return cur.value, peak.value
 
     def abort(self) -> None:
         if self._h is not None:

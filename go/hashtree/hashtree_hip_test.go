@@ -10,6 +10,7 @@ import (
 	"sync"
 	"testing"
 
+	"github.com/cbergoon/merkletree"
 	"github.com/stretchr/testify/assert"
 )
 
@@ -100,8 +101,53 @@ func TestPinnedBufferZeroCopy(t *testing.T) {
 	got, err := NewHashTreeFromBuffer(body, 1<<20)
 	assert.NoError(t, err)
 	assert.Equal(t, want.MerkleRoot(), got.MerkleRoot())
+	part, err := NewHashTreeFromPinned(b, len(body)-77, 1<<20)
+	assert.NoError(t, err)
+	wantPart, err := NewHashTreeFromBuffer(goCopy[:len(body)-77], 1<<20)
+	assert.NoError(t, err)
+	assert.Equal(t, wantPart.MerkleRoot(), part.MerkleRoot())
+	_, err = NewHashTreeFromPinned(b, len(body)+1, 1<<20)
+	assert.Error(t, err)
 	_, err = NewPinnedBuffer(0)
 	assert.Error(t, err)
+	b.Free()
+	b.Free() // idempotent
+	_, err = NewHashTreeFromPinned(b, 1, 1<<20)
+	assert.Error(t, err)
+}
+
+// cpuTree: the merkletree over crypto/sha256 leaf digests (Go's own hashing, no GPU).
+func cpuTree(t *testing.T, chunks [][]byte) *merkletree.MerkleTree {
+	list := make([]merkletree.Content, len(chunks))
+	for i, c := range chunks {
+		d := sha256.Sum256(c)
+		list[i] = HashTreeContent{digest: d[:]}
+	}
+	tree, err := merkletree.NewTree(list)
+	assert.NoError(t, err)
+	return tree
+}
+
+// More distinct chunk sizes than MaxBatchers: the extra sizes take dm_root_buffer, same trees.
+func TestBatcherBound(t *testing.T) {
+	body := make([]byte, 3<<20+5)
+	for i := range body {
+		body[i] = byte(i * 13)
+	}
+	for c := 1; c <= MaxBatchers+3; c++ {
+		chunk := c << 16
+		got, err := NewHashTreeFromBuffer(body, chunk)
+		assert.NoError(t, err)
+		var chunks [][]byte
+		for off := 0; off < len(body); off += chunk {
+			chunks = append(chunks, body[off:min(off+chunk, len(body))])
+		}
+		want := cpuTree(t, chunks)
+		assert.Equal(t, want.MerkleRoot(), got.MerkleRoot())
+	}
+	batchMu.Lock()
+	assert.LessOrEqual(t, len(batchers), MaxBatchers)
+	batchMu.Unlock()
 }
 
 // Concurrent handler goroutines (the batcher path) get the trees a single call gives.

@@ -3,13 +3,16 @@
 // Drop-in replacement for DeOSS common/hashtree/types.go (reference lines 19-39): the same
 // NewHashTree signature and errors, with leaf hashing and the root on the GPU through the
 // C ABI in include/deoss_merkle.h.  One process-wide context spans every GPU chosen by Init or
-// DEOSS_GPUS (default: all visible GPUs), so a large object or file list shards by aligned chunk
-// ranges across the node's GPUs with one RCCL all-gather of subtree roots.
+// DEOSS_GPUS (default: all visible GPUs).  Each call runs whole on the least-loaded GPU, so
+// concurrent handlers spread over the node (8 concurrent NewHashTree calls over 256 x 32 MiB
+// segment files: one GPU each, ~0.5 s together); a call is sharded by aligned chunk ranges with
+// one RCCL all-gather of subtree roots only when the library's cost model says it finishes sooner
+// and no other call is in flight (e.g. a 1 TiB object, or 1 MiB chunks bound by one PCIe link;
+// DESIGN.md §7).  Build: CGO_ENABLED=1, -tags hip, PKG_CONFIG_PATH=<checkout>/deoss_amd.
 package hashtree
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../deoss_amd -ldeoss_merkle -Wl,-rpath,${SRCDIR}/../../deoss_amd
+#cgo pkg-config: deoss_merkle
 #include <stdlib.h>
 #include "deoss_merkle.h"
 */
@@ -166,14 +169,20 @@ func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error) {
 // dm_batcher per chunk size, so concurrent handler goroutines share GPU passes instead of
 // queueing one chain-latency pass each on the context (DESIGN.md §6.9: 131x for 256 concurrent
 // 1 MiB uploads).  Larger objects take dm_root_buffer: ramped striped H2D overlapped with
-// hashing, zero-copy from pinned memory, sharded over the context's GPUs.
+// hashing, zero-copy from pinned memory, on the least-loaded GPU (or sharded, see above).
 const BatchLimit = 256 << 20
+
+// MaxBatchers bounds the batchers (each owns 2 worker contexts per GPU): the first MaxBatchers
+// distinct chunk sizes get one; calls with any other chunk size take dm_root_buffer.  DeOSS uses
+// one chunk size (chain.SegmentSize).
+const MaxBatchers = 4
 
 var (
 	batchMu  sync.Mutex
 	batchers = map[int]*C.dm_batcher{}
 )
 
+// batcherFor returns the chunk size's batcher, or nil when MaxBatchers other sizes hold one.
 func batcherFor(chunk int) (*C.dm_batcher, error) {
 	if _, err := gpu(); err != nil { // fixes the device list
 		return nil, err
@@ -182,6 +191,9 @@ func batcherFor(chunk int) (*C.dm_batcher, error) {
 	defer batchMu.Unlock()
 	if b, ok := batchers[chunk]; ok {
 		return b, nil
+	}
+	if len(batchers) >= MaxBatchers {
+		return nil, nil
 	}
 	devs, err := deviceList()
 	if err != nil {
@@ -215,11 +227,14 @@ func NewHashTreeFromBuffer(buf []byte, chunkSize int) (*merkletree.MerkleTree, e
 	n := (len(buf) + chunkSize - 1) / chunkSize
 	leaves := make([]byte, 32*n)
 	root := make([]byte, 32)
+	var b *C.dm_batcher
 	if len(buf) <= BatchLimit {
-		b, err := batcherFor(chunkSize)
-		if err != nil {
+		var err error
+		if b, err = batcherFor(chunkSize); err != nil {
 			return nil, err
 		}
+	}
+	if b != nil {
 		runtime.LockOSThread()
 		defer runtime.UnlockOSThread()
 		rc := C.dm_batcher_root(b, unsafe.Pointer(&buf[0]), C.uint64_t(len(buf)),

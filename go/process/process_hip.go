@@ -5,23 +5,24 @@
 // (node/objectHandler.go:168, node/fileHandler.go:771, node/filesHandler.go:201,
 // node/resumeHandler.go:326, node/tracker.go:767-769) and the fragment download path re-runs
 // (node/fileHandler.go:964,997).  Same signature and result shape; segmenting, Reed-Solomon 4 + 8
-// coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h): calls
-// from concurrent handler goroutines go through one dm_batcher, which coalesces whatever is
-// queued into one batched GPU pass (dm_batcher_process); files larger than one window (8
-// segments) go through dm_full_processing on a per-GPU pipeline, which reads the file, writes
-// every fragment and segment file itself and overlaps those writes with the GPU's coding and
-// hashing (one GPU pass per 32 GiB of file, no Go memory for the data).  Go memory of the small
-// path is bounded process-wide: 1 GiB per window in flight, DEOSS_PROCESS_MEM_GIB (default 8)
-// windows at once across every upload, buffers pooled.  Swap it in by changing the handlers' import of
-// github.com/CESSProject/cess-go-sdk/core/process to this package (INTEGRATION.md).
-// Deviation: cipher must be "" (the AES branch is not implemented; INTEGRATION.md).  Segment and
-// fragment files are both written to savedir under their hex SHA-256.  Build with `-tags hip`,
-// CGO_ENABLED=1.
+// coding, the SHA-256 names and the fid tree run on the MI355X (include/deoss_merkle.h):
+//   - files of up to one window (8 segments = 256 MiB), the common upload: one call through a
+//     process-wide dm_batcher, which coalesces whatever concurrent handler goroutines have queued
+//     into one batched GPU pass (dm_batcher_process); Go memory is bounded process-wide (1 GiB
+//     per call in flight, DEOSS_PROCESS_MEM_GIB (default 8) at once, buffers pooled);
+//   - larger files: dm_full_processing on a per-GPU pipeline, which reads the file, writes every
+//     fragment and segment file itself and overlaps those writes with the GPU's coding and hashing
+//     (one GPU pass per 32 GiB of file, no Go memory for the data);
+//   - cipher != "" (an encrypted upload, the Cipher header of node/objectHandler.go:102 and
+//     node/fileHandler.go:705): the SDK's own FullProcessing, unchanged -- its AES scheme is not
+//     restated here, so those uploads keep exactly the SDK's results.
+// Swap it in by changing the handlers' import of github.com/CESSProject/cess-go-sdk/core/process to
+// this package (INTEGRATION.md).  Segment and fragment files are both written to savedir under
+// their hex SHA-256.  Build with `-tags hip`, CGO_ENABLED=1, PKG_CONFIG_PATH=<checkout>/deoss_amd.
 package process
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../deoss_amd -ldeoss_merkle -Wl,-rpath,${SRCDIR}/../../deoss_amd
+#cgo pkg-config: deoss_merkle
 #include <stdlib.h>
 #include "deoss_merkle.h"
 */
@@ -40,17 +41,17 @@ import (
 	"unsafe"
 
 	"github.com/CESSProject/cess-go-sdk/chain"
+	sdkprocess "github.com/CESSProject/cess-go-sdk/core/process"
 )
 
-// windowSegments segments go to the GPU per call: 8 x 32 MiB of file plus 8 x 12 x 8 MiB of
-// fragments = 1 GiB of Go memory per window.  A large file runs several windows at once (they
-// meet in the same dm_batcher pass, so the GPU still sees one wide batch), and every window in
-// flight, across all goroutines, holds one slot of the process-wide memory budget.
+// windowSegments: files of up to this many segments go to the GPU in one batcher call (8 x 32 MiB
+// of file plus 8 x 12 x 8 MiB of fragments = 1 GiB of Go memory); every call in flight, across
+// all goroutines, holds one slot of the process-wide memory budget.  Larger files take
+// dm_full_processing (no Go memory for the data).
 const windowSegments = 8
 
 var (
 	once    sync.Once
-	ctx     *C.dm_ctx     // tree levels over the segment digests of multi-window files
 	batcher *C.dm_batcher // FullProcessing requests from every goroutine
 	initEr  error
 	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
@@ -80,11 +81,11 @@ func gpu() error {
 			return &windowBuf{data: make([]byte, windowSegments*seg), frags: make([]byte, windowSegments*total*frag),
 				segd: make([]byte, 32*windowSegments), fragd: make([]byte, 32*windowSegments*total)}
 		}
-		if rc := C.dm_create(&ctx, nil, 0); rc != C.DM_OK {
-			initEr = errors.New(C.GoString(C.dm_strerror(rc)))
+		ngpu := int(C.dm_gpu_count())
+		if ngpu <= 0 {
+			initEr = errors.New(C.GoString(C.dm_strerror(C.DM_ERR_NODEV)))
 			return
 		}
-		ngpu := int(C.dm_gpu_count())
 		pipes = make(chan *C.dm_rs, ngpu)
 		for g := 0; g < ngpu; g++ {
 			var pc *C.dm_ctx
@@ -122,24 +123,17 @@ func batcherError(rc C.int) error {
 	return errors.New(C.GoString(C.dm_strerror(rc)))
 }
 
-func ctxError(rc C.int) error {
-	if msg := C.GoString(C.dm_last_error(ctx)); msg != "" {
-		return errors.New(msg)
-	}
-	return errors.New(C.GoString(C.dm_strerror(rc)))
-}
-
-// window is one GPU call's worth of the file: segments [first, first+nseg).
+// window is one batcher call: the whole file, nseg <= windowSegments segments.
 type window struct {
-	first, nseg uint64
-	n           int // file bytes in the window
-	buf         *windowBuf
-	fid         [32]byte
-	err         error
+	nseg uint64
+	n    int // file bytes
+	buf  *windowBuf
+	fid  [32]byte
+	err  error
 }
 
-// runWindow reads the window's bytes at its file offset, codes + hashes them through the batcher
-// and writes its fragments to savedir; the caller holds one budget slot.
+// runWindow reads the file, codes + hashes it through the batcher and writes its fragments to
+// savedir; the caller holds one budget slot.
 func runWindow(f *os.File, w *window, savedir string) {
 	seg := uint64(chain.SegmentSize)
 	total := uint64(chain.DataShards + chain.ParShards)
@@ -147,7 +141,13 @@ func runWindow(f *os.File, w *window, savedir string) {
 	b := bufs.Get().(*windowBuf)
 	w.buf = b
 	data := b.data[:w.n]
-	if _, err := f.ReadAt(data, int64(w.first*seg)); err != nil && err != io.EOF {
+	// every byte must come from this file: a pooled buffer still holds an earlier upload's bytes,
+	// so a file shorter than its Stat size (truncated or rewritten since) is an error, as in
+	// dm_full_processing ("unexpected EOF"), never a silently stale tail
+	if n, err := f.ReadAt(data, 0); n != w.n {
+		if err == nil || err == io.EOF {
+			err = io.ErrUnexpectedEOF
+		}
 		w.err = err
 		return
 	}
@@ -191,8 +191,8 @@ func runWindow(f *os.File, w *window, savedir string) {
 // chain.DataShards + chain.ParShards fragments written to savedir/<hex SHA-256>, and returns the
 // segment / fragment path names and the fid (hex hashtree root over the segments).
 func FullProcessing(file string, cipher string, savedir string) ([]chain.SegmentDataInfo, string, error) {
-	if cipher != "" {
-		return nil, "", errors.New("process: cipher is not supported by the GPU pipeline")
+	if cipher != "" { // encrypted upload: the SDK's own pipeline (AES before coding), unchanged
+		return sdkprocess.FullProcessing(file, cipher, savedir)
 	}
 	if err := gpu(); err != nil {
 		return nil, "", err
@@ -214,69 +214,37 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		return nil, "", err
 	}
 	seg := uint64(chain.SegmentSize)
-	total := chain.DataShards + chain.ParShards
-	nsegAll := (size + seg - 1) / seg
-	if nsegAll > windowSegments {
-		return fullProcessingLarge(file, savedir, nsegAll)
+	total := uint64(chain.DataShards + chain.ParShards)
+	nseg := (size + seg - 1) / seg
+	if nseg > windowSegments {
+		return fullProcessingLarge(file, savedir, nseg)
 	}
-	var wins []*window
-	for first := uint64(0); first < nsegAll; first += windowSegments {
-		nseg := min(uint64(windowSegments), nsegAll-first)
-		wins = append(wins, &window{first: first, nseg: nseg, n: int(min(nseg*seg, size-first*seg))})
-	}
-	var wg sync.WaitGroup
-	for _, w := range wins { // windows run concurrently within the budget and batch together on the GPU
-		slots <- struct{}{}
-		wg.Add(1)
-		go func(w *window) {
-			defer wg.Done()
-			defer func() { <-slots }()
-			runWindow(f, w, savedir)
-		}(w)
-	}
-	wg.Wait()
-	info := make([]chain.SegmentDataInfo, 0, nsegAll)
-	segDigests := make([]byte, 0, 32*nsegAll)
-	var firstErr error
-	for _, w := range wins {
-		if w.err != nil && firstErr == nil {
-			firstErr = w.err
-		}
-		if firstErr == nil {
-			b := w.buf
-			for s := uint64(0); s < w.nseg; s++ {
-				names := make([]string, total)
-				for j := 0; j < total; j++ {
-					t := s*uint64(total) + uint64(j)
-					names[j] = filepath.Join(savedir, hex.EncodeToString(b.fragd[32*t:32*t+32]))
-				}
-				info = append(info, chain.SegmentDataInfo{
-					SegmentHash:  filepath.Join(savedir, hex.EncodeToString(b.segd[32*s:32*s+32])),
-					FragmentHash: names,
-				})
-			}
-			segDigests = append(segDigests, b.segd[:32*w.nseg]...)
-		}
+	w := &window{nseg: nseg, n: int(size)}
+	slots <- struct{}{}
+	runWindow(f, w, savedir)
+	<-slots
+	defer func() {
 		if w.buf != nil {
 			bufs.Put(w.buf)
-			w.buf = nil
 		}
+	}()
+	if w.err != nil {
+		return nil, "", w.err
 	}
-	if firstErr != nil {
-		return nil, "", firstErr
-	}
-	fid := wins[0].fid
-	if len(wins) > 1 { // several windows: the fid is the tree over every segment
-		nodes := make([]byte, 32*uint64(C.dm_tree_node_count(C.uint64_t(len(info)))))
-		runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
-		defer runtime.UnlockOSThread()
-		if rc := C.dm_tree_levels(ctx, (*C.uint8_t)(unsafe.Pointer(&segDigests[0])), C.uint64_t(len(info)),
-			(*C.uint8_t)(unsafe.Pointer(&nodes[0]))); rc != C.DM_OK {
-			return nil, "", ctxError(rc)
+	b := w.buf
+	info := make([]chain.SegmentDataInfo, 0, nseg)
+	for s := uint64(0); s < nseg; s++ {
+		names := make([]string, total)
+		for j := uint64(0); j < total; j++ {
+			t := s*total + j
+			names[j] = filepath.Join(savedir, hex.EncodeToString(b.fragd[32*t:32*t+32]))
 		}
-		copy(fid[:], nodes[len(nodes)-32:])
+		info = append(info, chain.SegmentDataInfo{
+			SegmentHash:  filepath.Join(savedir, hex.EncodeToString(b.segd[32*s:32*s+32])),
+			FragmentHash: names,
+		})
 	}
-	return info, hex.EncodeToString(fid[:]), nil
+	return info, hex.EncodeToString(w.fid[:]), nil
 }
 
 // fullProcessingLarge: one dm_full_processing call on a free per-GPU pipeline.  The library reads

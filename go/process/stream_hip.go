@@ -16,6 +16,7 @@ import (
 	"unsafe"
 
 	"github.com/CESSProject/cess-go-sdk/chain"
+	sdkprocess "github.com/CESSProject/cess-go-sdk/core/process"
 )
 
 // Writer is FullProcessing while the upload body arrives (dm_pstream_*, include/deoss_merkle.h).
@@ -25,14 +26,31 @@ import (
 // handler copies the body into io.MultiWriter(f, w): whole segments are copied to the GPU, coded,
 // hashed and their fragment files written to savedir while later bytes are still being received;
 // Close returns the same ([]chain.SegmentDataInfo, fid, error) as FullProcessing on the saved file.
-// A Writer is used by one goroutine; Close or Abort must be called exactly once.
+// A Writer is used by one goroutine; Close or Abort must be called exactly once.  Device memory
+// is bounded per Writer (DEOSS_PS_DEVICE_CAP, default 16 GiB), whatever the body size.
 type Writer struct {
 	st      *C.dm_pstream
 	savedir string
 	n       uint64
+	// an encrypted upload (NewWriterFor with a cipher): the bytes only go to the handler's file,
+	// and Close runs the SDK's FullProcessing(fpath, cipher, savedir) over it
+	sdkFile, sdkCipher string
+	sdkOpen            bool
 }
 
-// NewWriter opens a streaming FullProcessing into savedir (cipher "" only, like FullProcessing).
+// NewWriterFor is the handler-shaped form: fpath is the file the handler saves the body to (beside
+// this Writer, through io.MultiWriter), cipher its Cipher header.  With cipher "" it is NewWriter;
+// with a cipher the Writer only counts the bytes and Close returns the SDK's
+// FullProcessing(fpath, cipher, savedir) over the saved file -- the handler must have written and
+// closed fpath before Close.  So one code path serves plain and encrypted uploads.
+func NewWriterFor(fpath, cipher, savedir string) (*Writer, error) {
+	if cipher == "" {
+		return NewWriter(savedir)
+	}
+	return &Writer{savedir: savedir, sdkFile: fpath, sdkCipher: cipher, sdkOpen: true}, nil
+}
+
+// NewWriter opens a streaming FullProcessing into savedir (FullProcessing(fpath, "", savedir)).
 func NewWriter(savedir string) (*Writer, error) {
 	if err := gpu(); err != nil {
 		return nil, err
@@ -67,6 +85,10 @@ func lastError(rc C.int) error {
 
 // Write implements io.Writer.  The bytes are copied before it returns (p may be reused).
 func (w *Writer) Write(p []byte) (int, error) {
+	if w.sdkOpen {
+		w.n += uint64(len(p))
+		return len(p), nil
+	}
 	if w.st == nil {
 		return 0, errors.New("process: write on a closed Writer")
 	}
@@ -90,6 +112,10 @@ func (w *Writer) Write(p []byte) (int, error) {
 
 // Close finishes the last segment and returns FullProcessing's results for everything written.
 func (w *Writer) Close() ([]chain.SegmentDataInfo, string, error) {
+	if w.sdkOpen {
+		w.sdkOpen = false
+		return sdkprocess.FullProcessing(w.sdkFile, w.sdkCipher, w.savedir)
+	}
 	if w.st == nil {
 		return nil, "", errors.New("process: Writer already closed")
 	}
@@ -130,6 +156,7 @@ func (w *Writer) Close() ([]chain.SegmentDataInfo, string, error) {
 
 // Abort drops the stream; no file it started is left in savedir.
 func (w *Writer) Abort() {
+	w.sdkOpen = false
 	if w.st != nil {
 		C.dm_pstream_abort(w.st)
 		w.st = nil

@@ -10,8 +10,7 @@
 package reedsolomon
 
 /*
-#cgo CFLAGS: -I${SRCDIR}/../../include
-#cgo LDFLAGS: -L${SRCDIR}/../../deoss_amd -ldeoss_merkle -Wl,-rpath,${SRCDIR}/../../deoss_amd
+#cgo pkg-config: deoss_merkle
 #include <stdlib.h>
 #include "deoss_merkle.h"
 */

@@ -250,6 +250,12 @@ int dm_pstream_write(dm_pstream *st, const void *data, uint64_t len);
 int dm_pstream_close(dm_pstream *st, uint8_t *seg_hashes, uint8_t *frag_hashes, uint64_t cap, uint64_t *nseg_out,
                      uint8_t fid[32]);
 void dm_pstream_abort(dm_pstream *st);
+/* Device memory of a pstream: chunk buffers (segments + parity, 3x the body at 4 + 8) allocated now
+ * (in use or kept for reuse) and the most ever allocated.  A chunk's buffer is reused once its
+ * parity is written out and the leaf launch that hashed it has finished; at the cap
+ * (env DEOSS_PS_DEVICE_CAP, default 16 GiB) write blocks until the oldest one is free, so a
+ * stream's HBM does not grow with the body. */
+int dm_pstream_stats(dm_pstream *st, uint64_t *device_bytes, uint64_t *peak_device_bytes);
 
 /* ---- Merkle tree levels and proofs ----------------------------------------
  * cbergoon/merkletree v0.2.0 (go.mod:10) keeps every node of the tree NewHashTree returns

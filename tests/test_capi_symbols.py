@@ -72,3 +72,35 @@ def test_no_gpu_fails_loudly(lib):
         Processor()
     info, fid, err = FullProcessing(__file__, "", "/nonexistent-savedir")
     assert info is None and fid == "" and isinstance(err, DeossMerkleError)
+
+
+def test_pkg_config_file_points_at_this_checkout(lib):
+    """build() writes deoss_amd/deoss_merkle.pc for the Go packages' `#cgo pkg-config: deoss_merkle`:
+    its include directory holds the header, its library directory the built library, and every
+    Go package binds through it (no relative ${SRCDIR} paths that break when the files are copied
+    into DeOSS)."""
+    pc = os.path.join(ROOT, "deoss_amd", "deoss_merkle.pc")
+    vars_ = {}
+    fields = {}
+    for line in open(pc):
+        line = line.strip()
+        if "=" in line and ":" not in line.split("=")[0]:
+            k, v = line.split("=", 1)
+            vars_[k] = v
+        elif ":" in line:
+            k, v = line.split(":", 1)
+            fields[k.strip()] = v.strip()
+
+    def expand(v):
+        for _ in range(4):
+            for k, x in vars_.items():
+                v = v.replace("${" + k + "}", x)
+        return v
+    inc = expand(fields["Cflags"]).split("-I", 1)[1].split()[0]
+    libdir = expand(fields["Libs"]).split("-L", 1)[1].split()[0]
+    assert os.path.exists(os.path.join(inc, "deoss_merkle.h"))
+    assert os.path.exists(os.path.join(libdir, "libdeoss_merkle.so"))
+    assert "-ldeoss_merkle" in fields["Libs"]
+    for pkg in ("hashtree/types_hip.go", "process/process_hip.go", "reedsolomon/reedsolomon_hip.go"):
+        src = open(os.path.join(ROOT, "go", pkg)).read()
+        assert "#cgo pkg-config: deoss_merkle" in src and "${SRCDIR}" not in src, pkg

@@ -210,6 +210,34 @@ def test_processing_stream_small(ctx, oracle_lib, tmp_path, monkeypatch, slot, b
     p.close()
 
 
+@pytest.mark.parametrize("cap_bufs", [0, 1, 3])
+def test_processing_stream_device_cap(ctx, oracle_lib, tmp_path, monkeypatch, cap_bufs):
+    """a pstream's HBM must not grow with the body.  Chunk buffers (2 MiB each
+    here: 2 segments of 4 KiB + parity, rounded up) are reused once their parity is out and their
+    leaf launch has finished; at DEOSS_PS_DEVICE_CAP write blocks (launching the pending batch
+    early).  A body of 100 chunks through a cap of 0 (= one buffer), 1 and 3 buffers: peak device
+    bytes stay within the cap and the results equal the oracle's."""
+    from oracle import splitmix64_bytes
+    monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", "8192")
+    monkeypatch.setenv("DEOSS_PS_DEVICE_CAP", str(max(1, cap_bufs * (2 << 20))))   # 1 B: below one buffer
+    p = _processor(ctx, 4, 8, 4096)
+    n = 200 * 4096 - 77
+    data = splitmix64_bytes(n, 0xDE0552350 + cap_bufs)
+    st = p.NewProcessingStream(str(tmp_path / "cap"))
+    for piece in _pieces(data, random.Random(cap_bufs), 20000):
+        st.write(piece)
+        cur, peak = st.stats()
+        assert cur <= max(cap_bufs, 1) * (2 << 20) and peak <= max(cap_bufs, 1) * (2 << 20)
+    info, fid = st.close()
+    assert 0 < st.peak_device_bytes <= max(cap_bufs, 1) * (2 << 20)
+    seg_b, frag_b, want_fid, _ = oracle_lib.full_processing(data, 4096, 4, 8)
+    assert fid == want_fid.hex()
+    assert st.segment_digests == seg_b and st.fragment_digests == frag_b
+    assert len(info) == 200
+    assert not [x for x in os.listdir(tmp_path / "cap") if x.startswith(".")]
+    p.close()
+
+
 def test_processing_stream_full_segments_and_errors(ctx, oracle_lib, tmp_path):
     """32 MiB segments through dm_pstream in 1 B .. 3 MiB pieces = dm_full_processing on the same
     file = the oracle; two streams at once on one coder; empty and aborted streams leave nothing."""
