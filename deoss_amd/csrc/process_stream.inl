@@ -99,7 +99,10 @@ Dev& ps_dev(dm_pstream* st) { return st->r->c->devs[0]; }
 // A free slot (its H2D / D2H finished and its writes joined).  Slots are pinned on first use, so a
 // small body holds one slot, not four.
 int ps_take_slot(dm_pstream* st, int* out) {
-    const int sl = (int)(st->next_slot++ % kPsSlots);
+    int sl;
+    do {   // never the slot being filled / flushed (a drain inside ps_flush must not reuse it)
+        sl = (int)(st->next_slot++ % kPsSlots);
+    } while (sl == st->cur);
     if (!st->slot[sl].p) PSHIP(st->slot[sl].ensure(std::max(st->slot_len, st->spp * st->pbytes)));
     if (st->busy[sl]) {
         PSHIP(hipEventSynchronize(st->ev_slot[sl]));
@@ -114,6 +117,7 @@ int ps_take_slot(dm_pstream* st, int* out) {
 // Copy chunk ci's parity out through a slot and write its parity fragments (RS must be done).
 int ps_drain_chunk(dm_pstream* st, uint64_t ci) {
     PsChunk* ch = st->chunks[ci];
+    if (!ch->mem.p) return pfail(st, DM_ERR_INVALID, "pstream: draining a chunk without device memory");
     uint8_t* parity = ch->mem.u8() + ch->ns * st->seg;
     for (uint64_t t0 = 0; t0 < ch->ns; t0 += st->spp) {
         const uint64_t nt = std::min(st->spp, ch->ns - t0);
@@ -167,7 +171,11 @@ int ps_launch_batch(dm_pstream* st, uint64_t upto) {
     b->c0 = st->hashed_chunks;
     b->nc = upto - b->c0;
     b->s0 = st->chunks[b->c0]->s0;
-    for (uint64_t c = b->c0; c < upto; c++) b->ns += st->chunks[c]->ns;
+    for (uint64_t c = b->c0; c < upto; c++) {
+        if (!st->chunks[c]->mem.p)   // every chunk of a launch holds its data (host-side guard)
+            return pfail(st, DM_ERR_INVALID, "pstream: chunk without device memory in a leaf launch");
+        b->ns += st->chunks[c]->ns;
+    }
     const uint64_t T = b->ns * (1 + (uint64_t)st->total);
     PSHIP(b->htab.ensure(16 * T));
     PSHIP(b->tab.ensure(16 * T));
@@ -282,12 +290,16 @@ int ps_flush(dm_pstream* st) {
     const uint64_t ns = ceil_div(st->fill, st->seg), len = ns * st->seg;
     uint8_t* buf = st->slot[sl].u8();
     if (len > st->fill) std::memset(buf + st->fill, 0, len - st->fill);
+    // the buffer first: reclaiming may launch and drain every chunk already in the list, and a
+    // chunk joins the list only once it has memory (its H2D and RS follow right below)
+    DevBuf mem;
+    RC_TRY(ps_chunk_buffer(st, ns * (st->seg + st->pbytes), &mem));
     PsChunk* ch = new PsChunk();
-    st->chunks.push_back(ch);
-    ch->s0 = st->chunks.size() > 1 ? st->chunks[st->chunks.size() - 2]->s0 + st->chunks[st->chunks.size() - 2]->ns : 0;
+    ch->mem = mem;
+    ch->s0 = st->chunks.empty() ? 0 : st->chunks.back()->s0 + st->chunks.back()->ns;
     ch->ns = ns;
+    st->chunks.push_back(ch);
     PSHIP(hipEventCreateWithFlags(&ch->ev_rs, hipEventDisableTiming));
-    RC_TRY(ps_chunk_buffer(st, ns * (st->seg + st->pbytes), &ch->mem));
     PSHIP(hipMemcpyAsync(ch->mem.p, buf, len, hipMemcpyHostToDevice, st->copy));
     PSHIP(hipEventRecord(st->ev_slot[sl], st->copy));
     std::vector<FpFile> files;
