@@ -182,6 +182,8 @@ struct SlotWrites {
     ~SlotWrites() { (void)wait(); }
 };
 
+constexpr uint64_t kFpKeepBytes = 4ull << 30;   // window scratch kept between dm_full_processing calls
+
 struct FpEvents {
     hipEvent_t slot[kFpSlots] = {}, rs = nullptr, copied = nullptr;
     ~FpEvents() {
@@ -379,10 +381,17 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
     std::vector<uint8_t> segd(32 * nseg), fragd(32 * nseg * total);
     std::vector<std::pair<std::string, uint64_t>> pend;
     int rc = full_processing_windows(r, fs, dir, segment, flags, segd, fragd, pend, fid);
-    if (rc != DM_OK) {   // a failed call may leave copies queued: none may land in a slot the next call fills
+    {
         Dev& d = c->devs[0];
-        (void)hipStreamSynchronize(d.copy);
-        (void)hipStreamSynchronize(d.stream);
+        if (rc != DM_OK) {   // a failed call may leave copies queued: none may land in a slot the next call fills
+            (void)hipStreamSynchronize(d.copy);
+            (void)hipStreamSynchronize(d.stream);
+        }
+        // the window buffers grow with the file (up to 32 GiB of segments + 64 GiB of parity): give
+        // back what a large call took beyond kFpKeepBytes, so it does not stay resident beside
+        // other work on this GPU; the call has synchronised its streams already
+        if (d.data.cap > kFpKeepBytes) d.data.release();
+        if (r->work.cap > kFpKeepBytes) r->work.release();
     }
     for (size_t i = 0; rc == DM_OK && i < pend.size(); i++) {
         const uint64_t at = pend[i].second;

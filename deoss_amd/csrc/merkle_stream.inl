@@ -54,6 +54,7 @@ struct dm_stream {
     uint64_t launched = 0;   // leaves whose hashing is enqueued
     std::string err;
     int failed = DM_OK;      // sticky: after a failed write nothing more reaches the GPU; close returns it
+    Dev tree;                // the stream's own tree scratch (leaves, K2 nodes, root): close takes no context lock
 };
 
 namespace {
@@ -171,6 +172,7 @@ void stream_free(dm_stream* st) {
         b->htab.release();
         delete b;
     }
+    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) b->release();
     st->stage[0].release();
     st->stage[1].release();
     for (hipEvent_t e : {st->ev_stage[0], st->ev_stage[1], st->ev_copy})
@@ -200,6 +202,8 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     // load until the stream is freed, so concurrent uploads spread over the context's devices
     st->dev = pick_device(ctx);
     ctx->slots[st->dev].load++;
+    st->tree.id = ctx->devs[st->dev].id;
+    st->tree.cus = ctx->devs[st->dev].cus;
     st->chunk = chunk;
     st->seg_leaves = std::max<uint64_t>(1, (1ull << 30) / chunk);
     int rc = DM_OK;
@@ -317,17 +321,17 @@ int dm_stream_close(dm_stream* st, uint8_t* leaf_out, uint64_t leaf_cap, uint64_
         const uint64_t n = ceil_div(st->received, st->chunk);
         if ((rc = stream_launch(st, n, st->received - (n - 1) * st->chunk)) != DM_OK) break;
         if (nleaves) *nleaves = n;
-        // tree over all leaf digests on the context's stream, after every compute stream
-        CallLock lk(c, st->dev);
-        Dev& d = c->devs[st->dev];
-        hipStream_t s = d.stream;
-        if ((rc = begin_call(c, d, s)) != DM_OK) break;
-        for (int k = 0; k < kStreamLanes; k++) {
+        // tree over all leaf digests on the stream's first compute lane, after the other lane, in
+        // the stream's own scratch: no context lock, so a close never waits behind another call
+        Dev& d = st->tree;
+        hipStream_t s = st->comp[0];
+        for (int k = 1; k < kStreamLanes; k++) {
             hipError_t e = hipStreamWaitEvent(s, st->ev_comp[k], 0);
             if (e != hipSuccess) { rc = fail(c, DM_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e)); break; }
         }
         if (rc != DM_OK) break;
         hipError_t e = d.leaves.ensure(n * 32);
+        if (e == hipSuccess) e = d.root.ensure(32);
         if (e != hipSuccess) { rc = fail(c, DM_ERR_NOMEM, "leaf digests: %s", hipGetErrorString(e)); break; }
         for (StreamBatch* b : st->batches) {
             e = hipMemcpyAsync(d.leaves.u8() + 32 * b->first, b->digests.p, b->count * 32, hipMemcpyDeviceToDevice, s);

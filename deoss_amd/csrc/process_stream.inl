@@ -76,6 +76,7 @@ struct dm_pstream {
     std::vector<std::pair<std::string, uint64_t>> pend;   // temporary, digest index (~: segment)
     std::string err;
     int failed = DM_OK;   // sticky: after a failed write the stream only aborts (close returns this)
+    Dev tree;             // the stream's own fid scratch: close takes no context lock
 };
 
 namespace {
@@ -360,6 +361,7 @@ void ps_free(dm_pstream* st) {
         delete b;
     }
     for (auto& b : st->slot) b.release();
+    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) b->release();
     for (hipEvent_t e : st->ev_slot)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {st->ev_copy, st->ev_code})
@@ -536,13 +538,14 @@ int pstream_close(dm_pstream* st, uint8_t* seg_hashes, uint8_t* frag_hashes, uin
             if (!e.empty() && rc == DM_OK) rc = pfail(st, DM_ERR_IO, e);
         }
         if (rc != DM_OK) break;
-        {   // fid: the tree over every segment digest, on the context
-            CallLock lk(c, 0);
-            Dev& d = ps_dev(st);
-            hipStream_t s = d.stream;
-            if ((rc = begin_call(c, d, s)) != DM_OK) break;
+        {   // fid: the tree over every segment digest, in the stream's own scratch on its code stream
+            // (no context lock: a close never waits behind a dm_full_processing on the same GPU)
+            Dev& d = st->tree;
+            d.id = ps_dev(st).id;
+            d.cus = ps_dev(st).cus;
+            hipStream_t s = st->code;
             hipError_t e;
-            if ((e = d.leaves.ensure(32 * nseg)) != hipSuccess ||
+            if ((e = d.root.ensure(32)) != hipSuccess || (e = d.leaves.ensure(32 * nseg)) != hipSuccess ||
                 (e = hipMemcpyAsync(d.leaves.p, segd.data(), 32 * nseg, hipMemcpyHostToDevice, s)) != hipSuccess) {
                 rc = pfail(st, DM_ERR_HIP, std::string("fid: ") + hipGetErrorString(e));
                 break;
