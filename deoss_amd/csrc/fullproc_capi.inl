@@ -390,8 +390,8 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
         // the window buffers grow with the file (up to 32 GiB of segments + 64 GiB of parity): give
         // back what a large call took beyond kFpKeepBytes, so it does not stay resident beside
         // other work on this GPU; the call has synchronised its streams already
-        if (d.data.cap > kFpKeepBytes) d.data.release();
-        if (r->work.cap > kFpKeepBytes) r->work.release();
+        if (d.data.cap > kFpKeepBytes) c->reaper.put(d.id, d.data);
+        if (r->work.cap > kFpKeepBytes) c->reaper.put(d.id, r->work);
     }
     for (size_t i = 0; rc == DM_OK && i < pend.size(); i++) {
         const uint64_t at = pend[i].second;

@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdlib>
@@ -96,6 +98,83 @@ struct PinnedBuf {
     }
 };
 
+// Deferred release.  hipFree, hipFreeAsync and hipHostFree wait for ALL work queued on the device
+// (tools/free_sync_probe.hip, profiles/r03/free_sync_probe.log: ~280 ms behind an unrelated 300 ms
+// kernel on another stream; hipMalloc and event calls do not wait).  So buffers a call no longer
+// needs go to the context's reaper thread, which frees them in order: the caller never waits for
+// other callers' kernels.  The same device-wide wait makes it safe: every use of a buffer was
+// queued before the buffer was handed over.
+struct Reaper {
+    std::mutex mu;
+    std::condition_variable cv;
+    struct Item {
+        int dev;
+        void* p;
+        bool pinned;
+    };
+    std::deque<Item> q;
+    bool stop = false;
+    std::thread th;
+    void put(int dev, void* p, bool pinned) {
+        if (!p) return;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back({dev, p, pinned});
+            if (!th.joinable()) th = std::thread([this] { run(); });
+        }
+        cv.notify_one();
+    }
+    void put(int dev, DevBuf& b) {
+        put(dev, b.p, false);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    void put(int dev, PinnedBuf& b) {
+        put(dev, b.p, true);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    void run() {
+        for (;;) {
+            Item it;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return stop || !q.empty(); });
+                if (q.empty()) return;   // stop requested and drained
+                it = q.front();
+                q.pop_front();
+            }
+            if (hipSetDevice(it.dev) == hipSuccess) {
+                if (it.pinned) (void)hipHostFree(it.p);
+                else (void)hipFree(it.p);
+            }
+            (void)hipGetLastError();
+        }
+    }
+    void finish() {   // free everything queued, then end the thread (dm_destroy)
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_one();
+        if (th.joinable()) th.join();
+    }
+    ~Reaper() { finish(); }
+};
+
+// The HIP resources of one streaming upload (dm_stream / dm_pstream), pooled per device and reused
+// by the next stream: creating streams and pinning staging costs ~10 ms per object
+// (profiles/r03/free_sync_probe.log), and destroying / unpinning waits for the whole device.
+struct StreamKit {
+    static constexpr int kEvents = 10, kSlots = 4;
+    hipStream_t copy = nullptr;          // high priority: staging reuse never waits behind leaf kernels
+    hipStream_t code = nullptr, comp[2] = {nullptr, nullptr};
+    hipEvent_t ev[kEvents] = {};
+    PinnedBuf slot[kSlots];              // staging slots, pinned on first use
+    PinnedBuf tabs;                      // pinned arena for per-launch leaf tables
+    uint64_t tabs_used = 0;
+};
+
 struct Dev {
     int id = 0;
     int cus = 256;                      // compute units (leaf-kernel choice)
@@ -122,6 +201,8 @@ struct Dev {
 struct DevSlot {
     std::mutex mu;
     std::atomic<int> load{0};
+    std::mutex kit_mu;
+    std::vector<StreamKit*> kits;          // idle stream kits of this device
 };
 
 struct dm_ctx {
@@ -132,6 +213,7 @@ struct dm_ctx {
     std::map<int, std::vector<ncclComm_t>> comms;   // RCCL communicators over devices [0, G'), by G'
     std::mutex err_mu;
     std::string err;
+    Reaper reaper;                         // deferred hipFree / hipHostFree (never in a caller's path)
     bool timing = false;                   // written with every device locked
     std::atomic<int> leaf_mode{DM_LEAF_AUTO};
     // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-memory objects through the
@@ -270,6 +352,79 @@ int ctx_load(const dm_ctx* c) {
     int s = 0;
     for (size_t g = 0; g < c->devs.size(); g++) s += c->slots[g].load.load();
     return s;
+}
+
+void kit_destroy(StreamKit* k) {
+    for (hipStream_t s : {k->copy, k->code, k->comp[0], k->comp[1]})
+        if (s) {
+            (void)hipStreamSynchronize(s);
+            (void)hipStreamDestroy(s);
+        }
+    for (hipEvent_t e : k->ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& b : k->slot) b.release();
+    k->tabs.release();
+    delete k;
+}
+
+// A stream kit of device g (the caller has made g current): an idle one from the pool, else new.
+int kit_acquire(dm_ctx* c, int g, StreamKit** out) {
+    *out = nullptr;
+    DevSlot& sl = c->slots[g];
+    {
+        std::lock_guard<std::mutex> lk(sl.kit_mu);
+        if (!sl.kits.empty()) {
+            *out = sl.kits.back();
+            sl.kits.pop_back();
+            (*out)->tabs_used = 0;
+            return DM_OK;
+        }
+    }
+    StreamKit* k = new StreamKit();
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    hipError_t e = hipStreamCreateWithPriority(&k->copy, hipStreamNonBlocking, hi);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->code, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comp[0], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&k->comp[1], hipStreamNonBlocking);
+    for (int i = 0; i < StreamKit::kEvents && e == hipSuccess; i++)
+        e = hipEventCreateWithFlags(&k->ev[i], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        kit_destroy(k);
+        return fail(c, DM_ERR_HIP, "stream kit: %s", hipGetErrorString(e));
+    }
+    *out = k;
+    return DM_OK;
+}
+
+// Back to device g's pool; the caller has synchronised the kit's streams (its own work only).
+void kit_release(dm_ctx* c, int g, StreamKit* k) {
+    if (!k) return;
+    DevSlot& sl = c->slots[g];
+    std::lock_guard<std::mutex> lk(sl.kit_mu);
+    sl.kits.push_back(k);
+}
+
+// `bytes` of the kit's pinned table arena (leaf tables uploaded by later H2D copies).  A full
+// arena is replaced, and the old one goes to the reaper: copies still queued may read it.
+uint8_t* kit_table(dm_ctx* c, int dev, StreamKit* k, uint64_t bytes) {
+    bytes = round_up(std::max<uint64_t>(bytes, 1), 256);
+    if (k->tabs_used + bytes > k->tabs.cap) {
+        const uint64_t want = std::max<uint64_t>({bytes, 2 * k->tabs.cap, 1ull << 20});
+        c->reaper.put(dev, k->tabs);
+        if (k->tabs.ensure(want) != hipSuccess) return nullptr;
+        k->tabs_used = 0;
+    }
+    uint8_t* p = k->tabs.u8() + k->tabs_used;
+    k->tabs_used += bytes;
+    return p;
+}
+
+// Grow a pinned buffer to n bytes without waiting on the device: the old one goes to the reaper.
+hipError_t pinned_grow(dm_ctx* c, int dev, PinnedBuf& b, uint64_t n) {
+    if (n <= b.cap) return hipSuccess;
+    c->reaper.put(dev, b);
+    return b.ensure(n);
 }
 
 // Device holding device memory p (device-resident entry points run where their data lives);
@@ -1163,6 +1318,12 @@ void dm_destroy(dm_ctx* ctx) {
     DeviceRestore dev;
     for (auto& kv : ctx->comms)
         for (auto& cm : kv.second) (void)ncclCommDestroy(cm);
+    for (size_t g = 0; g < ctx->devs.size() && ctx->slots; g++) {
+        if (hipSetDevice(ctx->devs[g].id) != hipSuccess) continue;
+        for (StreamKit* k : ctx->slots[g].kits) kit_destroy(k);
+        ctx->slots[g].kits.clear();
+    }
+    ctx->reaper.finish();
     for (auto& d : ctx->devs) destroy_device(d);
     delete ctx;
 }

@@ -27,7 +27,6 @@ struct StreamBatch {
     uint64_t first = 0, count = 0;
     DevBuf tab;       // count x (address, length)
     DevBuf digests;   // count x 32 bytes
-    PinnedBuf htab;   // host side of tab (kept until the launch has run)
 };
 
 }  // namespace
@@ -35,6 +34,7 @@ struct StreamBatch {
 struct dm_stream {
     dm_ctx* c = nullptr;
     int dev = 0;
+    StreamKit* kit = nullptr;   // pooled streams, events, staging (borrowed for the stream's life)
     uint64_t chunk = 0;
     uint64_t seg_leaves = 0;
     std::vector<StreamSeg*> segs;
@@ -94,10 +94,11 @@ int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
     bt->first = st->launched;
     bt->count = upto - st->launched;
     const uint64_t n = bt->count;
-    SHIP(bt->htab.ensure(16 * n));
+    uint8_t* htab = kit_table(st->c, st->c->devs[st->dev].id, st->kit, 16 * n);   // host side of tab
+    if (!htab) return sfail(st, DM_ERR_NOMEM, "pinned table arena", hipErrorOutOfMemory);
     SHIP(bt->tab.ensure(16 * n));
     SHIP(bt->digests.ensure(32 * n));
-    uint64_t* h = reinterpret_cast<uint64_t*>(bt->htab.p);
+    uint64_t* h = reinterpret_cast<uint64_t*>(htab);
     for (uint64_t j = 0; j < n; j++) {
         const uint64_t leaf = bt->first + j;
         StreamSeg* g;
@@ -110,7 +111,7 @@ int stream_launch(dm_stream* st, uint64_t upto, uint64_t last_len) {
     const int k = st->next_comp++ % kStreamLanes;
     hipStream_t s = st->comp[k];
     SHIP(hipStreamWaitEvent(s, st->ev_copy, 0));
-    SHIP(hipMemcpyAsync(bt->tab.p, bt->htab.p, 16 * n, hipMemcpyHostToDevice, s));
+    SHIP(hipMemcpyAsync(bt->tab.p, htab, 16 * n, hipMemcpyHostToDevice, s));
     dm::LeafArgs la{};
     la.addrs = static_cast<const uint64_t*>(bt->tab.p);
     la.lens = la.addrs + n;
@@ -155,33 +156,33 @@ int stream_flush(dm_stream* st) {
     return DM_OK;
 }
 
+// End of a stream: wait for its own work only, hand its device buffers to the reaper (freeing
+// them here would wait for every other caller's kernels on the device) and its kit back to the pool.
 void stream_free(dm_stream* st) {
     if (!st) return;
-    st->c->slots[st->dev].load--;   // the stream's hold on its device's load (dm_stream_open)
-    (void)hipSetDevice(st->c->devs[st->dev].id);
-    if (st->copy) (void)hipStreamSynchronize(st->copy);
-    for (int k = 0; k < kStreamLanes; k++)
-        if (st->comp[k]) (void)hipStreamSynchronize(st->comp[k]);
+    dm_ctx* c = st->c;
+    const int id = c->devs[st->dev].id;
+    (void)hipSetDevice(id);
+    bool idle = true;
+    if (st->kit)
+        for (hipStream_t s : {st->copy, st->comp[0], st->comp[1]})
+            if (s && hipStreamSynchronize(s) != hipSuccess) idle = false;
     for (StreamSeg* g : st->segs) {
-        g->data.release();
+        c->reaper.put(id, g->data);
         delete g;
     }
     for (StreamBatch* b : st->batches) {
-        b->tab.release();
-        b->digests.release();
-        b->htab.release();
+        c->reaper.put(id, b->tab);
+        c->reaper.put(id, b->digests);
         delete b;
     }
-    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) b->release();
-    st->stage[0].release();
-    st->stage[1].release();
-    for (hipEvent_t e : {st->ev_stage[0], st->ev_stage[1], st->ev_copy})
-        if (e) (void)hipEventDestroy(e);
-    for (int k = 0; k < kStreamLanes; k++) {
-        if (st->ev_comp[k]) (void)hipEventDestroy(st->ev_comp[k]);
-        if (st->comp[k]) (void)hipStreamDestroy(st->comp[k]);
+    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) c->reaper.put(id, *b);
+    if (st->kit) {
+        for (int i = 0; i < 2; i++) st->kit->slot[i] = st->stage[i];
+        if (idle) kit_release(c, st->dev, st->kit);
+        else kit_destroy(st->kit);   // a failed stream's kit is not reused
     }
-    if (st->copy) (void)hipStreamDestroy(st->copy);
+    c->slots[st->dev].load--;   // the stream's hold on its device's load (dm_stream_open)
     delete st;
 }
 
@@ -210,26 +211,26 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     do {
         hipError_t e;
         if ((e = hipSetDevice(ctx->devs[st->dev].id)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "hipSetDevice", e); break; }
-        // copies on a high-priority stream (its own hardware queue): staging reuse must not wait
-        // behind long leaf kernels
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((e = hipStreamCreateWithPriority(&st->copy, hipStreamNonBlocking, hi)) != hipSuccess) { rc = sfail(st, DM_ERR_HIP, "stream", e); break; }
-        for (int k = 0; k < kStreamLanes && rc == DM_OK; k++) {
-            if ((e = hipStreamCreateWithFlags(&st->comp[k], hipStreamNonBlocking)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&st->ev_comp[k], hipEventDisableTiming)) != hipSuccess)
-                rc = sfail(st, DM_ERR_HIP, "stream", e);
-        }
-        if (rc != DM_OK) break;
-        if ((e = hipEventCreateWithFlags(&st->ev_copy, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&st->ev_stage[0], hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&st->ev_stage[1], hipEventDisableTiming)) != hipSuccess) {
-            rc = sfail(st, DM_ERR_HIP, "event", e);
+        if ((rc = kit_acquire(ctx, st->dev, &st->kit)) != DM_OK) {
+            st->err = t_err;
             break;
         }
-        if ((e = st->stage[0].ensure(kStreamStage)) != hipSuccess || (e = st->stage[1].ensure(kStreamStage)) != hipSuccess) {
-            rc = sfail(st, DM_ERR_NOMEM, "pinned staging", e);
-            break;
+        StreamKit* k = st->kit;
+        st->copy = k->copy;   // copies on the kit's high-priority stream (its own hardware queue)
+        for (int i = 0; i < kStreamLanes; i++) {
+            st->comp[i] = k->comp[i];
+            st->ev_comp[i] = k->ev[1 + i];
+        }
+        st->ev_copy = k->ev[0];
+        st->ev_stage[0] = k->ev[3];
+        st->ev_stage[1] = k->ev[4];
+        for (int i = 0; i < 2; i++) {
+            st->stage[i] = k->slot[i];
+            k->slot[i] = PinnedBuf();
+            if ((e = pinned_grow(ctx, ctx->devs[st->dev].id, st->stage[i], kStreamStage)) != hipSuccess) {
+                rc = sfail(st, DM_ERR_NOMEM, "pinned staging", e);
+                break;
+            }
         }
     } while (0);
     if (rc != DM_OK) {

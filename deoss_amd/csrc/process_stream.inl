@@ -25,6 +25,7 @@
 namespace {
 
 constexpr int kPsSlots = 4;
+static_assert(kPsSlots == StreamKit::kSlots && StreamKit::kEvents >= 2 + kPsSlots, "pstream kit layout");
 constexpr uint64_t kPsSlotBytes = 64ull << 20;
 constexpr uint64_t kPsBatchChunks = 32;   // 64 segments = 2 GiB of body per leaf launch (32 MiB segments)
 // Device bytes one pstream may hold: two 6 GiB batches in flight (32 chunks x 2 segments x 96 MiB)
@@ -44,7 +45,6 @@ struct PsChunk {
 struct PsBatch {
     uint64_t c0 = 0, nc = 0, s0 = 0, ns = 0;   // chunks [c0, c0 + nc) = segments [s0, s0 + ns)
     DevBuf tab, dig;                            // leaf table; digests: ns segments, then ns x total fragments
-    PinnedBuf htab;
     int lane = 0;
     hipEvent_t ev_done = nullptr;               // the leaf launch has finished reading its chunks
 };
@@ -53,6 +53,7 @@ struct PsBatch {
 
 struct dm_pstream {
     dm_rs* r = nullptr;
+    StreamKit* kit = nullptr;   // pooled streams, events, pinned slots (borrowed for the stream's life)
     int k = 0, m = 0, total = 0, flags = 0;
     uint64_t seg = 0, frag = 0, pbytes = 0, spd = 1, spp = 1, slot_len = 0, batch_chunks = kPsBatchChunks;
     std::string dir, base;
@@ -104,7 +105,7 @@ int ps_take_slot(dm_pstream* st, int* out) {
     do {   // never the slot being filled / flushed (a drain inside ps_flush must not reuse it)
         sl = (int)(st->next_slot++ % kPsSlots);
     } while (sl == st->cur);
-    if (!st->slot[sl].p) PSHIP(st->slot[sl].ensure(std::max(st->slot_len, st->spp * st->pbytes)));
+    PSHIP(pinned_grow(st->r->c, ps_dev(st).id, st->slot[sl], std::max(st->slot_len, st->spp * st->pbytes)));
     if (st->busy[sl]) {
         PSHIP(hipEventSynchronize(st->ev_slot[sl]));
         const std::string e = st->wr[sl].wait();
@@ -178,10 +179,11 @@ int ps_launch_batch(dm_pstream* st, uint64_t upto) {
         b->ns += st->chunks[c]->ns;
     }
     const uint64_t T = b->ns * (1 + (uint64_t)st->total);
-    PSHIP(b->htab.ensure(16 * T));
+    uint8_t* htab = kit_table(st->r->c, d.id, st->kit, 16 * T);   // host side of the leaf table
+    if (!htab) return pfail(st, DM_ERR_NOMEM, "pstream: pinned table arena");
     PSHIP(b->tab.ensure(16 * T));
     PSHIP(b->dig.ensure(32 * T));
-    uint64_t* addr = reinterpret_cast<uint64_t*>(b->htab.p);
+    uint64_t* addr = reinterpret_cast<uint64_t*>(htab);
     uint64_t* lens = addr + T;
     uint64_t i = 0;
     for (uint64_t c = b->c0; c < upto; c++) {
@@ -208,7 +210,7 @@ int ps_launch_batch(dm_pstream* st, uint64_t upto) {
     // lanes overlap, so one batch's segment chains run while the next batch arrives
     PSHIP(hipEventRecord(st->ev_code, st->code));
     PSHIP(hipStreamWaitEvent(s, st->ev_code, 0));
-    PSHIP(hipMemcpyAsync(b->tab.p, b->htab.p, 16 * T, hipMemcpyHostToDevice, s));
+    PSHIP(hipMemcpyAsync(b->tab.p, htab, 16 * T, hipMemcpyHostToDevice, s));
     dm::LeafArgs la{};
     la.addrs = static_cast<const uint64_t*>(b->tab.p);
     la.lens = la.addrs + T;
@@ -271,7 +273,7 @@ int ps_chunk_buffer(dm_pstream* st, uint64_t bytes, DevBuf* out) {
         if (!st->spare.empty()) {   // spare buffers too small for this chunk: give them back first
             for (auto& b : st->spare) {
                 st->dev_held -= b.cap;
-                b.release();
+                st->r->c->reaper.put(ps_dev(st).id, b);
             }
             st->spare.clear();
             continue;
@@ -341,33 +343,38 @@ int ps_flush(dm_pstream* st) {
     return DM_OK;
 }
 
+// End of a pstream: wait for its own streams only, hand its device buffers to the reaper (a
+// hipFree here would wait for every other caller's kernels on the GPU) and its kit to the pool.
 void ps_free(dm_pstream* st) {
     if (!st) return;
-    (void)hipSetDevice(ps_dev(st).id);
-    for (hipStream_t s : {st->copy, st->code, st->comp[0], st->comp[1]})
-        if (s) (void)hipStreamSynchronize(s);
+    dm_ctx* c = st->r->c;
+    const int id = ps_dev(st).id;
+    (void)hipSetDevice(id);
+    bool idle = true;
+    if (st->kit)
+        for (hipStream_t s : {st->copy, st->code, st->comp[0], st->comp[1]})
+            if (s && hipStreamSynchronize(s) != hipSuccess) idle = false;
     for (auto& w : st->wr) (void)w.wait();
     for (PsChunk* ch : st->chunks) {
-        ch->mem.release();
+        c->reaper.put(id, ch->mem);
         if (ch->ev_rs) (void)hipEventDestroy(ch->ev_rs);
         delete ch;
     }
-    for (auto& b : st->spare) b.release();
+    for (auto& b : st->spare) c->reaper.put(id, b);
     for (PsBatch* b : st->batches) {
-        b->tab.release();
-        b->dig.release();
-        b->htab.release();
+        c->reaper.put(id, b->tab);
+        c->reaper.put(id, b->dig);
         if (b->ev_done) (void)hipEventDestroy(b->ev_done);
         delete b;
     }
-    for (auto& b : st->slot) b.release();
-    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) b->release();
-    for (hipEvent_t e : st->ev_slot)
-        if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {st->ev_copy, st->ev_code})
-        if (e) (void)hipEventDestroy(e);
-    for (hipStream_t s : {st->copy, st->code, st->comp[0], st->comp[1]})
-        if (s) (void)hipStreamDestroy(s);
+    for (DevBuf* b : {&st->tree.leaves, &st->tree.nodes_a, &st->tree.nodes_b, &st->tree.root}) c->reaper.put(id, *b);
+    if (st->kit) {
+        for (int i = 0; i < kPsSlots; i++) st->kit->slot[i] = st->slot[i];
+        if (idle) kit_release(c, 0, st->kit);
+        else kit_destroy(st->kit);   // a failed stream's kit is not reused
+    } else {
+        for (auto& b : st->slot) c->reaper.put(id, b);
+    }
     delete st;
 }
 
@@ -417,22 +424,22 @@ int dm_pstream_open(dm_rs* r, uint64_t segment, const char* savedir, int flags, 
     do {
         const std::string me = mkdir_all(st->dir);
         if (!me.empty()) { rc = pfail(st, DM_ERR_IO, me); break; }
-        hipError_t e;
-        if ((e = hipSetDevice(ps_dev(st).id)) != hipSuccess) { rc = pfail(st, DM_ERR_HIP, "hipSetDevice"); break; }
-        int lo = 0, hi = 0;
-        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-        if ((e = hipStreamCreateWithPriority(&st->copy, hipStreamNonBlocking, hi)) != hipSuccess ||
-            (e = hipStreamCreateWithFlags(&st->code, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipStreamCreateWithFlags(&st->comp[0], hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipStreamCreateWithFlags(&st->comp[1], hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&st->ev_copy, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&st->ev_code, hipEventDisableTiming)) != hipSuccess) {
-            rc = pfail(st, DM_ERR_HIP, std::string("stream: ") + hipGetErrorString(e));
+        if (hipSetDevice(ps_dev(st).id) != hipSuccess) { rc = pfail(st, DM_ERR_HIP, "hipSetDevice"); break; }
+        if ((rc = kit_acquire(c, 0, &st->kit)) != DM_OK) {
+            st->err = t_err;
             break;
         }
-        for (int i = 0; i < kPsSlots && rc == DM_OK; i++) {
-            if ((e = hipEventCreateWithFlags(&st->ev_slot[i], hipEventDisableTiming)) != hipSuccess)
-                rc = pfail(st, DM_ERR_HIP, std::string("events: ") + hipGetErrorString(e));
+        StreamKit* k = st->kit;
+        st->copy = k->copy;   // H2D / D2H on the kit's high-priority stream
+        st->code = k->code;
+        st->comp[0] = k->comp[0];
+        st->comp[1] = k->comp[1];
+        st->ev_copy = k->ev[0];
+        st->ev_code = k->ev[1];
+        for (int i = 0; i < kPsSlots; i++) {
+            st->ev_slot[i] = k->ev[2 + i];
+            st->slot[i] = k->slot[i];   // pinned on first use (ps_take_slot)
+            k->slot[i] = PinnedBuf();
         }
     } while (0);
     if (rc != DM_OK) {
