@@ -33,6 +33,7 @@ struct FdGuard {
     }
 };
 constexpr uint64_t kFpWindowBytes = 32ull << 30;        // file bytes per GPU pass (+ 2x parity in HBM)
+constexpr uint64_t kFpStripeMinSegs = 4;                // windows of at least this many segments read in stripes
 
 std::atomic<uint64_t> g_fp_seq{0};
 
@@ -194,6 +195,115 @@ struct FpEvents {
     }
 };
 
+// Striped pass over one window of ns segments (file bytes [fbeg, fend)): for every stripe [o, o + w)
+// of the segment (stripe_schedule, split at fragment boundaries) the window's ns pieces are pread
+// into one pinned slot, copied to HBM with one 2D copy (segment pitch), and two resumable leaf
+// launches absorb them: the ns segment chains (kit->comp[0]) and the ns chains of the data fragment
+// the stripe lies in (kit->comp[1]).  After the last stripe: RS over the window and one leaf launch
+// over the parity fragments (on s), then the fid over the segment digests.  d.leaves: segment t at
+// t, data fragment (t, q) at ns * (1 + q) + t, parity fragment (t, i) at ns * (1 + k) + t * m + i.
+template <class TakeSlot>
+int fp_striped_pass(dm_rs* r, Dev& d, hipStream_t s, StreamKit* kit, const FileSet& fs, uint64_t fbeg, uint64_t fend,
+                    uint64_t ns, uint64_t seg, uint64_t slot_cap, int readers, TakeSlot& take_slot,
+                    bool (&busy)[kFpSlots], FpEvents& ev, uint8_t* parity, uint8_t* dfid, FpTrace& tr) {
+    dm_ctx* c = r->c;
+    const int k = r->k, m = r->m;
+    const uint64_t frag = seg / (uint64_t)k;
+    const uint64_t W = std::max<uint64_t>(64, (slot_cap / ns) / 64 * 64);   // slot row pitch
+    std::vector<uint64_t> so0, sw0, so, sw;
+    stripe_schedule(W, seg, so0, sw0);
+    for (size_t j = 0; j < so0.size(); j++)   // no stripe crosses a fragment boundary
+        for (uint64_t o = so0[j], e = std::min(seg, so0[j] + sw0[j]); o < e;) {
+            const uint64_t b = std::min(e, (o / frag + 1) * frag);
+            so.push_back(o);
+            sw.push_back(b - o);
+            o = b;
+        }
+    const uint64_t nsteps = so.size();
+    uint32_t* seg_state = reinterpret_cast<uint32_t*>(dfid + 256);
+    uint32_t* frag_state = seg_state + 8 * ns;
+    // tables: row j = the ns segment pointers at stripe j's offset; lens = ns segments, ns fragments;
+    // the parity launch: ns x m fragment pointers and lengths
+    std::vector<uint64_t> addr(nsteps * ns), lens(2 * ns, seg), paddr(ns * m), plen(ns * m, frag);
+    for (uint64_t t = 0; t < ns; t++) lens[ns + t] = frag;
+    for (uint64_t j = 0; j < nsteps; j++)
+        for (uint64_t t = 0; t < ns; t++) addr[j * ns + t] = reinterpret_cast<uint64_t>(d.data.u8() + t * seg + so[j]);
+    for (uint64_t i = 0; i < ns * m; i++) paddr[i] = reinterpret_cast<uint64_t>(parity + i * frag);
+    RC_TRY(tables_begin(c, d, (addr.size() + lens.size() + 2 * ns * m) * 8 + 4096));
+    HIP_TRY(d.leaves.ensure(32 * ns * (1 + (uint64_t)(k + m))));
+    RC_TRY(upload(c, d, s, d.tab_addr, addr.data(), addr.size() * 8));
+    RC_TRY(upload(c, d, s, d.tab_len, lens.data(), lens.size() * 8));
+    RC_TRY(upload(c, d, s, d.tab_first, paddr.data(), paddr.size() * 8));
+    RC_TRY(upload(c, d, s, d.tab_ids, plen.data(), plen.size() * 8));
+    HIP_TRY(hipEventRecord(ev.copied, s));   // the tables are on the device before any launch
+    for (hipStream_t x : {kit->comp[0], kit->comp[1]}) HIP_TRY(hipStreamWaitEvent(x, ev.copied, 0));
+    const int kind = pick_leaf_kernel(c, d, ns);
+    for (uint64_t j = 0; j < nsteps; j++) {
+        const uint64_t o = so[j], w = sw[j], q = o / frag;
+        int sl;
+        RC_TRY(take_slot(&sl));
+        uint8_t* buf = r->fp_slot[sl].u8();
+        std::vector<FilePart> parts;
+        for (uint64_t t = 0; t < ns; t++) {
+            const uint64_t a = fbeg + t * seg + o;
+            const uint64_t have = a < fend ? std::min(w, fend - a) : 0;
+            if (have) parts.push_back({0, a, have, buf + t * W});
+            if (have < w) std::memset(buf + t * W + have, 0, w - have);   // the last segment's zero padding
+        }
+        RC_TRY(read_parts(c, fs, parts, readers));
+        HIP_TRY(hipMemcpy2DAsync(d.data.u8() + o, seg, buf, W, w, ns, hipMemcpyHostToDevice, d.copy));
+        HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
+        busy[sl] = true;
+        dm::LeafArgs la{};
+        la.addrs = static_cast<const uint64_t*>(d.tab_addr.p) + j * ns;
+        la.nleaves = ns;
+        la.byte_off = o;
+        la.byte_end = o + w;
+        la.state = seg_state;
+        la.lens = static_cast<const uint64_t*>(d.tab_len.p);
+        la.digests = d.leaves.u8();
+        HIP_TRY(hipStreamWaitEvent(kit->comp[0], ev.slot[sl], 0));
+        RC_TRY(launch_leaves(c, d, kit->comp[0], la, true, true, kind));
+        la.byte_off = o - q * frag;
+        la.byte_end = la.byte_off + w;
+        la.state = frag_state;   // re-initialised where each fragment starts (byte_off 0)
+        la.lens = static_cast<const uint64_t*>(d.tab_len.p) + ns;
+        la.digests = d.leaves.u8() + 32 * ns * (1 + q);
+        HIP_TRY(hipStreamWaitEvent(kit->comp[1], ev.slot[sl], 0));
+        RC_TRY(launch_leaves(c, d, kit->comp[1], la, true, true, kind));
+    }
+    tr.mark("A': stripes read, launched");
+    // RS after the last copy, then the parity fragments' chains (8 MiB: shorter than the segments')
+    HIP_TRY(hipEventRecord(ev.copied, d.copy));
+    HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
+    dm::RsArgs a{};
+    for (int j = 0; j < k; j++) a.in[j] = d.data.u8() + (uint64_t)j * frag;
+    for (int i = 0; i < m; i++) a.out[i] = parity + (uint64_t)i * frag;
+    a.in_seg_stride = seg;
+    a.out_seg_stride = (uint64_t)m * frag;
+    a.units_per_seg = frag / 16;
+    a.nseg = ns;
+    a.table = static_cast<const uint2*>(r->enc_tab.p);
+    a.nout = (uint32_t)m;
+    launch_rs(d, s, k, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(ev.rs, s));
+    dm::LeafArgs pa{};
+    pa.addrs = static_cast<const uint64_t*>(d.tab_first.p);
+    pa.lens = static_cast<const uint64_t*>(d.tab_ids.p);
+    pa.nleaves = ns * m;
+    pa.byte_end = ~0ull;
+    pa.digests = d.leaves.u8() + 32 * ns * (1 + (uint64_t)k);
+    RC_TRY(launch_leaves(c, d, s, pa, true, true, pick_leaf_kernel(c, d, ns * m)));
+    // the fid once the segment chains are done
+    HIP_TRY(hipEventRecord(kit->ev[0], kit->comp[0]));
+    HIP_TRY(hipEventRecord(kit->ev[1], kit->comp[1]));
+    HIP_TRY(hipStreamWaitEvent(s, kit->ev[0], 0));
+    HIP_TRY(hipStreamWaitEvent(s, kit->ev[1], 0));
+    RC_TRY(finish(c, d, s, d.leaves.u8(), ns, true, dfid));
+    return DM_OK;
+}
+
 // Everything but the renames; `pend` collects (temporary name, digest slot) of every file written.
 int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir, uint64_t seg, int flags,
                             std::vector<uint8_t>& segd, std::vector<uint8_t>& fragd,
@@ -246,39 +356,68 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         return DM_OK;
     };
     const bool one_window = nseg <= win;
+    const char* stripes_env = std::getenv("DEOSS_FP_STRIPES");
+    const bool stripes_off = stripes_env != nullptr && stripes_env[0] == '0';
+    // two extra compute streams for the striped pass (segment and data-fragment chains side by side)
+    StreamKit* kit = nullptr;
+    RC_TRY(kit_acquire(c, 0, &kit));
+    struct KitBack {
+        dm_ctx* c;
+        StreamKit* k;
+        ~KitBack() {
+            for (hipStream_t x : {k->comp[0], k->comp[1]}) (void)hipStreamSynchronize(x);
+            kit_release(c, 0, k);
+        }
+    } kit_back{c, kit};
     FpTrace tr;
     for (uint64_t w0 = 0; w0 < nseg; w0 += win) {
         const uint64_t ns = std::min(win, nseg - w0);
         const uint64_t fbeg = w0 * seg, fend = std::min(size, (w0 + ns) * seg);
+        // striped (round 3): the window is read in stripes [o, o + w) of EVERY segment, so the segment
+        // and data-fragment chains start with the first stripe instead of after the whole window
+        // (the reads of an 8 GiB file took 236 ms before any chain started); needs whole 64-B blocks
+        // per fragment.  DEOSS_FP_STRIPES=0 keeps the read-then-launch order (A/B).
+        const bool striped = ns >= kFpStripeMinSegs && frag % 64 == 0 && !stripes_off;
         HIP_TRY(d.data.ensure(ns * seg + kAlign));
-        HIP_TRY(r->work.ensure(ns * pbytes + 32));
+        HIP_TRY(r->work.ensure(ns * pbytes + 256 + 2 * ns * 32));
         uint8_t* parity = r->work.u8();
         uint8_t* dfid = parity + ns * pbytes;
-        // A: file -> slots -> HBM, nothing else, so the leaf chains start as early as the reads allow
-        for (uint64_t t0 = 0; t0 < ns; t0 += spd) {
-            const uint64_t nt = std::min(spd, ns - t0), len = nt * seg, a = fbeg + t0 * seg;
-            int sl;
-            RC_TRY(take_slot(&sl));
-            uint8_t* buf = r->fp_slot[sl].u8();
-            const uint64_t have = a < fend ? std::min(len, fend - a) : 0;
-            std::vector<FilePart> parts;
-            for (uint64_t q = 0; q < have; q += 8ull << 20)
-                parts.push_back({0, a + q, std::min<uint64_t>(8ull << 20, have - q), buf + q});
-            RC_TRY(read_parts(c, fs, parts, readers));
-            if (have < len) std::memset(buf + have, 0, len - have);
-            HIP_TRY(hipMemcpyAsync(d.data.u8() + t0 * seg, buf, len, hipMemcpyHostToDevice, d.copy));
-            HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
-            busy[sl] = true;
-            if (t0 + nt == ns && have < len) {   // the file's last, zero-padded segment: keep a copy
-                tail.assign(buf + (nt - 1) * seg, buf + nt * seg);
-                tail_seg = w0 + t0 + nt - 1;
+        if (!striped) {
+            // A: file -> slots -> HBM, nothing else, so the leaf chains start as early as the reads allow
+            for (uint64_t t0 = 0; t0 < ns; t0 += spd) {
+                const uint64_t nt = std::min(spd, ns - t0), len = nt * seg, a = fbeg + t0 * seg;
+                int sl;
+                RC_TRY(take_slot(&sl));
+                uint8_t* buf = r->fp_slot[sl].u8();
+                const uint64_t have = a < fend ? std::min(len, fend - a) : 0;
+                std::vector<FilePart> parts;
+                for (uint64_t q = 0; q < have; q += 8ull << 20)
+                    parts.push_back({0, a + q, std::min<uint64_t>(8ull << 20, have - q), buf + q});
+                RC_TRY(read_parts(c, fs, parts, readers));
+                if (have < len) std::memset(buf + have, 0, len - have);
+                HIP_TRY(hipMemcpyAsync(d.data.u8() + t0 * seg, buf, len, hipMemcpyHostToDevice, d.copy));
+                HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
+                busy[sl] = true;
+                if (t0 + nt == ns && have < len) {   // the file's last, zero-padded segment: keep a copy
+                    tail.assign(buf + (nt - 1) * seg, buf + nt * seg);
+                    tail_seg = w0 + t0 + nt - 1;
+                }
+            }
+            tr.mark("A: reads + H2D enqueued");
+            // B: RS + one leaf launch over segments and fragments, after the last H2D
+            HIP_TRY(hipEventRecord(ev.copied, d.copy));
+            HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
+            RC_TRY(process_segments(r, d, s, d.data.u8(), seg, parity, {0, ns}, dfid, ev.rs));
+        } else {
+            RC_TRY(fp_striped_pass(r, d, s, kit, fs, fbeg, fend, ns, seg, slot_cap, readers, take_slot, busy, ev,
+                                   parity, dfid, tr));
+            if (fend - fbeg < ns * seg) {   // the file's last, zero-padded segment, for its data files
+                tail.assign(seg, 0);
+                const uint64_t a = fbeg + (ns - 1) * seg;
+                RC_TRY(read_parts(c, fs, {{0, a, fend - a, tail.data()}}, readers));
+                tail_seg = w0 + ns - 1;
             }
         }
-        tr.mark("A: reads + H2D enqueued");
-        // B: RS + one leaf launch over segments and fragments, after the last H2D
-        HIP_TRY(hipEventRecord(ev.copied, d.copy));
-        HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
-        RC_TRY(process_segments(r, d, s, d.data.u8(), seg, parity, {0, ns}, dfid, ev.rs));
         // C: while the leaf chains run, the data fragments and segment files are copied from the
         // file itself (copy_file_range: page cache to page cache), and the parity comes back
         // through the slots and is written as each set lands
@@ -326,12 +465,28 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             busy[sl] = true;
         }
         tr.mark("C: parity back, writes queued");
-        // D: digests (d.leaves: segment t at t, fragment (t, j) at ns + t * total + j)
-        HIP_TRY(hipMemcpyAsync(segd.data() + 32 * w0, d.leaves.p, 32 * ns, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(fragd.data() + 32 * w0 * total, d.leaves.u8() + 32 * ns, 32 * ns * total,
-                               hipMemcpyDeviceToHost, s));
+        // D: digests.  One pass: d.leaves holds segment t at t, fragment (t, j) at ns + t * total + j.
+        // Striped: segment t at t, data fragment (t, q) at ns * (1 + q) + t, parity fragment (t, i)
+        // at ns * (1 + k) + t * m + i (interleaved here)
+        std::vector<uint8_t> lv;
+        if (striped) {
+            lv.resize(32 * ns * (1 + (uint64_t)total));
+            HIP_TRY(hipMemcpyAsync(lv.data(), d.leaves.p, lv.size(), hipMemcpyDeviceToHost, s));
+        } else {
+            HIP_TRY(hipMemcpyAsync(segd.data() + 32 * w0, d.leaves.p, 32 * ns, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(fragd.data() + 32 * w0 * total, d.leaves.u8() + 32 * ns, 32 * ns * total,
+                                   hipMemcpyDeviceToHost, s));
+        }
         if (one_window) HIP_TRY(hipMemcpyAsync(fid, dfid, 32, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        if (striped) {
+            std::memcpy(segd.data() + 32 * w0, lv.data(), 32 * ns);
+            for (uint64_t t = 0; t < ns; t++)
+                for (int j = 0; j < total; j++) {
+                    const uint64_t from = j < k ? ns * (1 + (uint64_t)j) + t : ns * (1 + (uint64_t)k) + t * m + (j - k);
+                    std::memcpy(fragd.data() + 32 * ((w0 + t) * total + j), lv.data() + 32 * from, 32);
+                }
+        }
         HIP_TRY(hipStreamSynchronize(d.copy));   // this window's slots are in host memory: HBM reusable
         tr.mark("D: leaf pass done");
         const std::string e = wd.wait();

@@ -100,7 +100,9 @@ def test_process_errors(ctx):
 
 
 @pytest.mark.parametrize("path,slot,window", [("windows", None, None), ("one_call", None, None),
-                                              ("one_call", 8192, 3 * 4096), ("one_call", 3 * 4096, 4 * 4096)])
+                                              ("one_call_nostripes", None, None), ("one_call", 8192, 3 * 4096),
+                                              ("one_call", 3 * 4096, 4 * 4096), ("one_call", 8192, 6 * 4096),
+                                              ("one_call", 2 * 4096, 40 * 4096)])
 def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch, path, slot, window):
     """FullProcessing(file, "", savedir): fragment (and segment) files named by their SHA-256 with
     the right bytes, fid = oracle fid.  "windows": the window path (several dm_process_buffer
@@ -110,6 +112,9 @@ def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch, path, slo
     import deoss_amd.process as proc
     from oracle import splitmix64_bytes
     monkeypatch.setattr(proc, "WINDOW_SEGMENTS", 3)
+    if path == "one_call_nostripes":
+        monkeypatch.setenv("DEOSS_FP_STRIPES", "0")
+        path = "one_call"
     if slot:
         monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", str(slot))
         monkeypatch.setenv("DEOSS_FP_WINDOW_BYTES", str(window))
@@ -149,11 +154,15 @@ def test_full_processing_files(ctx, oracle_lib, tmp_path, monkeypatch, path, slo
     p.close()
 
 
-@pytest.mark.parametrize("nbytes", [1, 9 * (32 << 20) + 12345])
-def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, nbytes):
+@pytest.mark.parametrize("nbytes,stripes", [(1, "1"), (9 * (32 << 20) + 12345, "1"), (9 * (32 << 20) + 12345, "0"),
+                                            (4 * (32 << 20), "1"), (5 * (32 << 20) - 64, "1")])
+def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, monkeypatch, nbytes, stripes):
     """dm_full_processing at chain.SegmentSize (32 MiB segments, 4 + 8 fragments of 8 MiB): digests
-    and fid = the oracle's, every file on disk hashes to its name."""
+    and fid = the oracle's, every file on disk hashes to its name.  stripes "1": windows of >= 4
+    segments are read in stripes with the segment and data-fragment chains running from the first
+    stripe (round 3); "0": the read-then-launch order."""
     from oracle import splitmix64_bytes
+    monkeypatch.setenv("DEOSS_FP_STRIPES", stripes)
     p = _processor(ctx)
     data = splitmix64_bytes(nbytes, 0xDE0552200 + nbytes)
     f = tmp_path / "object.bin"
@@ -165,8 +174,10 @@ def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, nbyte
     names = sorted(os.listdir(savedir))
     assert names == sorted({fragd[32 * t:32 * t + 32].hex() for t in range(len(fragd) // 32)} |
                            {segd[32 * s:32 * s + 32].hex() for s in range(len(segd) // 32)})
-    for n in names[:6]:
+    for n in names[:6] + names[-3:]:
         assert hashlib.sha256(open(savedir / n, "rb").read()).hexdigest() == n
+    last = segd[-32:].hex()   # the zero-padded last segment's file
+    assert hashlib.sha256(open(savedir / last, "rb").read()).hexdigest() == last
     p.close()
 
 
