@@ -355,6 +355,30 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         *out = sl;
         return DM_OK;
     };
+    // The window's data fragments and segment files -- plain file bytes -- are copied from the
+    // file itself by background jobs (copy_file_range: page cache to page cache); the zero-padded
+    // last segment's from `tail`.
+    auto start_data_files = [&](uint64_t w0, uint64_t ns) {
+        std::vector<FpFile> files;
+        for (uint64_t gs = w0; gs < w0 + ns; gs++) {
+            const bool padded = gs == tail_seg;
+            auto add = [&](uint64_t off_in_seg, uint64_t len, const std::string& tmp) {
+                if (padded) files.push_back({tail.data() + off_in_seg, len, tmp});
+                else if (mem) files.push_back({mem + gs * seg + off_in_seg, len, tmp});
+                else files.push_back({nullptr, len, tmp, in_fd, gs * seg + off_in_seg});
+            };
+            for (int j = 0; j < k; j++) {
+                const uint64_t id = gs * (uint64_t)total + (uint64_t)j;
+                add((uint64_t)j * frag, frag, base + "f" + std::to_string(id));
+                pend.emplace_back(files.back().tmp, 32 * id);
+            }
+            if (flags & DM_FP_SEGMENT_FILES) {
+                add(0, seg, base + "s" + std::to_string(gs));
+                pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
+            }
+        }
+        wd.start(std::move(files), (size_t)env_bytes("DEOSS_FP_DATA_WRITERS", kFpDataWriters));
+    };
     const bool one_window = nseg <= win;
     const char* stripes_env = std::getenv("DEOSS_FP_STRIPES");
     const bool stripes_off = stripes_env != nullptr && stripes_env[0] == '0';
@@ -409,39 +433,20 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             HIP_TRY(hipStreamWaitEvent(s, ev.copied, 0));
             RC_TRY(process_segments(r, d, s, d.data.u8(), seg, parity, {0, ns}, dfid, ev.rs));
         } else {
-            RC_TRY(fp_striped_pass(r, d, s, kit, fs, fbeg, fend, ns, seg, slot_cap, readers, take_slot, busy, ev,
-                                   parity, dfid, tr));
             if (fend - fbeg < ns * seg) {   // the file's last, zero-padded segment, for its data files
                 tail.assign(seg, 0);
                 const uint64_t a = fbeg + (ns - 1) * seg;
                 RC_TRY(read_parts(c, fs, {{0, a, fend - a, tail.data()}}, readers));
                 tail_seg = w0 + ns - 1;
             }
+            // the data files need only the file: their copies run from the start, beside the reads
+            start_data_files(w0, ns);
+            RC_TRY(fp_striped_pass(r, d, s, kit, fs, fbeg, fend, ns, seg, slot_cap, readers, take_slot, busy, ev,
+                                   parity, dfid, tr));
         }
-        // C: while the leaf chains run, the data fragments and segment files are copied from the
-        // file itself (copy_file_range: page cache to page cache), and the parity comes back
-        // through the slots and is written as each set lands
-        {
-            std::vector<FpFile> files;
-            for (uint64_t gs = w0; gs < w0 + ns; gs++) {
-                const bool padded = gs == tail_seg;
-                auto add = [&](uint64_t off_in_seg, uint64_t len, const std::string& tmp) {
-                    if (padded) files.push_back({tail.data() + off_in_seg, len, tmp});
-                    else if (mem) files.push_back({mem + gs * seg + off_in_seg, len, tmp});
-                    else files.push_back({nullptr, len, tmp, in_fd, gs * seg + off_in_seg});
-                };
-                for (int j = 0; j < k; j++) {
-                    const uint64_t id = gs * (uint64_t)total + (uint64_t)j;
-                    add((uint64_t)j * frag, frag, base + "f" + std::to_string(id));
-                    pend.emplace_back(files.back().tmp, 32 * id);
-                }
-                if (flags & DM_FP_SEGMENT_FILES) {
-                    add(0, seg, base + "s" + std::to_string(gs));
-                    pend.emplace_back(files.back().tmp, ~(32 * gs));   // ~: a segment digest
-                }
-            }
-            wd.start(std::move(files), (size_t)env_bytes("DEOSS_FP_DATA_WRITERS", kFpDataWriters));
-        }
+        // C: while the leaf chains run, the parity comes back through the slots and is written as
+        // each set lands (the data fragments and segment files are already being copied)
+        if (!striped) start_data_files(w0, ns);
         HIP_TRY(hipStreamWaitEvent(d.copy, ev.rs, 0));
         tr.mark("B: launched, data copies started");
         for (uint64_t t0 = 0; t0 < ns; t0 += spp) {
