@@ -51,15 +51,24 @@ uint32_t ceil_log2(uint64_t n) {
 }
 uint64_t ceil_shift(uint64_t n, uint32_t k) { return k >= 64 ? (n ? 1 : 0) : (n + (1ull << k) - 1) >> k; }
 
+struct Reaper;
+void reaper_put(Reaper* r, int dev, void* p, bool pinned);
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    Reaper* rp = nullptr;   // set (context scratch): growth hands the old buffer to the context's reaper
+    int dev = -1;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) {
-            hipError_t e = hipDeviceSynchronize();   // scratch may still be in use by queued work
-            if (e != hipSuccess) return e;
-            (void)hipFree(p);
+            if (rp) {   // freed once the work queued so far has finished; this caller does not wait
+                reaper_put(rp, dev, p, false);
+            } else {
+                hipError_t e = hipDeviceSynchronize();   // scratch may still be in use by queued work
+                if (e != hipSuccess) return e;
+                (void)hipFree(p);
+            }
             p = nullptr;
             cap = 0;
         }
@@ -161,6 +170,8 @@ struct Reaper {
     }
     ~Reaper() { finish(); }
 };
+
+void reaper_put(Reaper* r, int dev, void* p, bool pinned) { r->put(dev, p, pinned); }
 
 // The HIP resources of one streaming upload (dm_stream / dm_pstream), pooled per device and reused
 // by the next stream: creating streams and pinning staging costs ~10 ms per object
@@ -966,6 +977,11 @@ int root_device_impl(dm_ctx* c, Dev& d, hipStream_t s, const void* dev, uint64_t
 
 int init_device(dm_ctx* c, Dev& d) {
     HIP_TRY(hipSetDevice(d.id));
+    for (DevBuf* b : {&d.data, &d.nodes_a, &d.nodes_b, &d.leaves, &d.tab_addr, &d.tab_len, &d.tab_first, &d.tab_ids,
+                      &d.root, &d.gather, &d.proof_paths, &d.proof_bits, &d.proof_roots}) {
+        b->rp = &c->reaper;   // scratch growth never synchronises the device (Reaper)
+        b->dev = d.id;
+    }
     HIP_TRY(hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id));
     HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));

@@ -204,6 +204,10 @@ int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
         }
     const std::vector<uint64_t> tab = rs_table(r->mat.data() + (size_t)k * k, parity_shards, k);
     Dev& d = ctx->devs[0];
+    for (DevBuf* b : {&r->enc_tab, &r->dec_tab, &r->work}) {
+        b->rp = &ctx->reaper;   // growth (r->work: FullProcessing windows) never synchronises the device
+        b->dev = d.id;
+    }
     hipError_t e = hipSetDevice(d.id);
     if (e == hipSuccess) e = r->enc_tab.ensure(tab.size() * 8);
     if (e == hipSuccess) e = hipMemcpy(r->enc_tab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
