@@ -230,6 +230,11 @@ struct dm_ctx {
     // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-memory objects through the
     // multi-device path (partition, RCCL all-gather, compaction, finish) even with one device.
     bool force_sharded = false;
+    // Test hook (env DEOSS_VIRTUAL_DEVICES=N at dm_create): N context devices on the first GPU, each
+    // with its own streams, scratch and lock, so routing, range locks, multi_root's partition and
+    // compaction and the batch split run with G = N on a one-GPU box.  RCCL rejects duplicate
+    // GPUs, so the gather of subtree roots is then a D2D copy to device 0 (real GPUs: RCCL).
+    bool virtual_devs = false;
 };
 
 namespace {
@@ -446,7 +451,10 @@ int device_of(dm_ctx* c, const void* p) {
     int g = 0;
     if (hipPointerGetAttributes(&attr, p) == hipSuccess)
         for (size_t i = 0; i < c->devs.size(); i++)
-            if (c->devs[i].id == attr.device) g = (int)i;
+            if (c->devs[i].id == attr.device) {
+                g = (int)i;
+                break;
+            }
     (void)hipGetLastError();
     return g;
 }
@@ -1054,7 +1062,7 @@ int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_
     const uint32_t k = P.k;
     const uint64_t nb = P.nb, maxc = P.max_nodes();
     std::vector<ncclComm_t>* comms = nullptr;
-    RC_TRY(comms_for(c, G, &comms));
+    if (!c->virtual_devs) RC_TRY(comms_for(c, G, &comms));
     // order this call's scratch use after every call still queued on another stream of each device
     for (int g = 0; g < G; g++) RC_TRY(begin_call(c, c->devs[g], c->devs[g].stream));
     std::vector<int> rcs(G, DM_OK);
@@ -1107,12 +1115,21 @@ int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_
         }
     // C1: all-gather of fixed-size slots (maxc nodes of 32 B per device) over RCCL
     const size_t slot = maxc * 32;
-    NCCL_TRY(ncclGroupStart());
-    for (int g = 0; g < G; g++) {
-        Dev& d = c->devs[g];
-        NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream));
+    if (c->virtual_devs) {   // test hook: every context device is the same GPU (no RCCL), see dm_ctx
+        for (int g = 0; g < G; g++) {
+            Dev& d = c->devs[g];
+            HIP_TRY(hipMemcpyAsync(c->devs[0].gather.u8() + slot + g * slot, d.gather.p, slot, hipMemcpyDeviceToDevice,
+                                   d.stream));
+        }
+        for (int g = 0; g < G; g++) HIP_TRY(hipStreamSynchronize(c->devs[g].stream));
+    } else {
+        NCCL_TRY(ncclGroupStart());
+        for (int g = 0; g < G; g++) {
+            Dev& d = c->devs[g];
+            NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream));
+        }
+        NCCL_TRY(ncclGroupEnd());
     }
-    NCCL_TRY(ncclGroupEnd());
     Dev& d0 = c->devs[0];
     HIP_TRY(hipSetDevice(d0.id));
     // compact the gathered slots into block order on device 0, in d0.leaves (K2's scratch is
@@ -1304,6 +1321,9 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
         for (size_t j = 0; j < i; j++)
             if (ids[j] == ids[i]) return bad_arg();
     }
+    const char* vd = std::getenv("DEOSS_VIRTUAL_DEVICES");   // test hook (dm_ctx::virtual_devs)
+    const int nvirt = vd ? std::atoi(vd) : 0;
+    if (nvirt > 1) ids.assign((size_t)std::min(nvirt, 64), ids[0]);
     dm_ctx* c = new dm_ctx();
     c->devs.resize(ids.size());
     c->slots.reset(new DevSlot[ids.size()]);
@@ -1317,7 +1337,8 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     }
     const char* fs = std::getenv("DEOSS_FORCE_SHARDED");
     c->force_sharded = fs != nullptr && fs[0] == '1';
-    if (ids.size() > 1 || c->force_sharded) {   // every device's communicator up front: fail here, not mid-call
+    c->virtual_devs = nvirt > 1;
+    if ((ids.size() > 1 || c->force_sharded) && !c->virtual_devs) {   // every device's communicator up front: fail here, not mid-call
         std::vector<ncclComm_t>* cm = nullptr;
         const int rc = comms_for(c, (int)ids.size(), &cm);
         if (rc != DM_OK) {

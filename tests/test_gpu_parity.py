@@ -436,6 +436,91 @@ def test_single_process_sharded_path(oracle_lib):
         c.close()
 
 
+def _virtual_context(n, sharded):
+    """DEOSS_VIRTUAL_DEVICES test hook: a context of n devices that are all this box's one GPU,
+    each with its own streams, scratch and lock (RCCL replaced by a D2D gather; dm_ctx)."""
+    from deoss_amd import MerkleContext
+    os.environ["DEOSS_VIRTUAL_DEVICES"] = str(n)
+    if sharded:
+        os.environ["DEOSS_FORCE_SHARDED"] = "1"
+    try:
+        return MerkleContext()
+    finally:
+        os.environ.pop("DEOSS_VIRTUAL_DEVICES", None)
+        os.environ.pop("DEOSS_FORCE_SHARDED", None)
+
+
+@pytest.mark.parametrize("G", [2, 3, 8])
+def test_virtual_devices_sharded_paths(oracle_lib, tmp_path, G):
+    """The multi-device code with G context devices on one GPU: multi_root's partition
+    (dm_plan::plan_shards), per-device leaf producers, the gather, compaction in block order and
+    the final levels, for host buffers (odd / even n, striped and packed), chunk lists and files;
+    batches split by objects over the devices (batch_host_multi).  Everything vs the oracle."""
+    c = _virtual_context(G, sharded=True)
+    try:
+        assert c.device_count() == G
+        for length, chunk in [(1000 * 4096 + 7, 4096), (3 * 64, 64), (257 * 1000, 1000), ((1 << 20) + 3, 1 << 14),
+                              ((300 << 20) + 5, 32 << 20), (17 * 4096, 4096)]:
+            host = oracle_lib.splitmix_bytes(length, length + G)
+            lw, want = oracle_lib.root_buffer(host, chunk, nthreads=8)
+            leaves, root = c.root_buffer(host, chunk, want_leaves=True)
+            assert root == want, (G, length, chunk)
+            assert leaves == lw, (G, length, chunk)
+        chunks = [oracle_lib.splitmix_bytes((777 * i) % 50001, 300 + i) for i in range(301)]
+        lw, want = oracle_lib.root_chunks(chunks, nthreads=8)
+        assert c.root_chunks(chunks) == (lw, want)
+        datas = [oracle_lib.splitmix_bytes(20000 + 37 * i, 900 + i) for i in range(40)]
+        paths = _write_files(tmp_path, datas, f"v{G}_")
+        lw, want = oracle_lib.root_chunks(datas, nthreads=8)
+        leaves, root = c.new_hash_tree(paths)
+        assert root == want and b"".join(leaves) == lw
+        objs = [oracle_lib.splitmix_bytes(1000 + 4099 * i, 50 + i) for i in range(3 * G + 1)]
+        roots = c.root_batch(objs, 4096)
+        assert roots == [oracle_lib.root_buffer(o, 4096)[1] for o in objs]
+    finally:
+        c.close()
+
+
+def test_virtual_devices_concurrent_routing(oracle_lib):
+    """Per-device locks and least-busy routing: 16 threads mixing host buffers, chunk lists,
+    streams and batches on a 4-device context (one GPU) get the oracle's roots."""
+    import threading
+    c = _virtual_context(4, sharded=False)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(4):
+                data = oracle_lib.splitmix_bytes(100000 + 7919 * (4 * t + i), 7000 + 4 * t + i)
+                want = oracle_lib.root_buffer(data, 8192)[1]
+                kind = (t + i) % 4
+                if kind == 0:
+                    got = c.root_buffer(data, 8192, want_leaves=False)[1]
+                elif kind == 1:
+                    got = c.root_chunks([data[o:o + 8192] for o in range(0, len(data), 8192)])[1]
+                elif kind == 2:
+                    st = c.open_stream(8192)
+                    st.write(data[:5000])
+                    st.write(data[5000:])
+                    got = st.close()[1]
+                else:
+                    got = c.root_batch([data, data[:3000]], 8192)[0]
+                if got != want:
+                    errors.append((t, i, kind))
+        except Exception as e:   # reported below
+            errors.append((t, repr(e)))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert errors == []
+    finally:
+        c.close()
+
+
 def _write_files(tmp_path, datas, tag):
     paths = []
     for i, d in enumerate(datas):
