@@ -458,7 +458,7 @@ def test_virtual_devices_sharded_paths(oracle_lib, tmp_path, G):
     batches split by objects over the devices (batch_host_multi).  Everything vs the oracle."""
     c = _virtual_context(G, sharded=True)
     try:
-        assert c.device_count() == G
+        assert c.device_count == G
         for length, chunk in [(1000 * 4096 + 7, 4096), (3 * 64, 64), (257 * 1000, 1000), ((1 << 20) + 3, 1 << 14),
                               ((300 << 20) + 5, 32 << 20), (17 * 4096, 4096)]:
             host = oracle_lib.splitmix_bytes(length, length + G)
