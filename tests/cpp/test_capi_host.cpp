@@ -618,6 +618,62 @@ int main(int argc, char** argv) {
         for (auto& x : ups) x.join();
     }
 
+    // round 3: four context devices on this one GPU (DEOSS_VIRTUAL_DEVICES): per-device locks,
+    // least-busy routing, pooled stream kits and the reaper under 8 threads mixing host buffers,
+    // streams (some aborted) and batches, then sharded calls over the four devices (forced)
+    {
+        setenv("DEOSS_VIRTUAL_DEVICES", "4", 1);
+        dm_ctx* cv = nullptr;
+        EXPECT(dm_create(&cv, nullptr, 0) == DM_OK);
+        setenv("DEOSS_FORCE_SHARDED", "1", 1);
+        dm_ctx* cvs = nullptr;
+        EXPECT(dm_create(&cvs, nullptr, 0) == DM_OK);
+        unsetenv("DEOSS_FORCE_SHARDED");
+        unsetenv("DEOSS_VIRTUAL_DEVICES");
+        if (cv && cvs) {
+            EXPECT(dm_device_count(cv) == 4);
+            std::vector<std::thread> vt;
+            for (int t = 0; t < 8; t++)
+                vt.emplace_back([cv, t] {
+                    for (int i = 0; i < 3; i++) {
+                        switch ((t + i) % 3) {
+                            case 0: check_buffer(cv, 150000 + 4099 * (3 * t + i), 8192, 1300 + 3 * t + i); break;
+                            case 1: go_stream_sequence(cv, 2000000 + 777 * t, 65536, 1400 + t, (t + i) % 5 == 0); break;
+                            default: {
+                                std::vector<std::vector<uint8_t>> objs;
+                                for (int o = 0; o < 5; o++) objs.push_back(bytes(30000 + 1000 * o + t, 1500 + 10 * t + o));
+                                std::vector<const void*> op;
+                                std::vector<uint64_t> ol;
+                                for (auto& o : objs) {
+                                    op.push_back(o.data());
+                                    ol.push_back(o.size());
+                                }
+                                std::vector<uint8_t> roots(32 * objs.size());
+                                EXPECT(dm_root_batch(cv, op.data(), ol.data(), objs.size(), 4096, roots.data()) == DM_OK);
+                                for (size_t o = 0; o < objs.size(); o++) {
+                                    uint8_t r[32];
+                                    EXPECT(or_root_buffer(objs[o].data(), objs[o].size(), 4096, nullptr, r, 1) == 0);
+                                    EXPECT(std::memcmp(r, roots.data() + 32 * o, 32) == 0);
+                                }
+                            }
+                        }
+                    }
+                });
+            for (auto& x : vt) x.join();
+            for (auto [len, chunk] : {std::pair<uint64_t, uint64_t>{777ull * 4096 + 5, 4096}, {(100ull << 20) + 3, 8ull << 20}}) {
+                auto b = bytes(len, len + 5);
+                const uint64_t n = (len + chunk - 1) / chunk;
+                std::vector<uint8_t> lw(32 * n), lg(32 * n);
+                uint8_t rw[32], rg[32];
+                EXPECT(or_root_buffer(b.data(), len, chunk, lw.data(), rw, 4) == 0);
+                EXPECT(dm_root_buffer(cvs, b.data(), len, chunk, lg.data(), rg) == DM_OK);
+                EXPECT(std::memcmp(rw, rg, 32) == 0 && lw == lg);
+            }
+        }
+        dm_destroy(cv);
+        dm_destroy(cvs);
+    }
+
     // concurrent callers on one context
     std::vector<std::thread> th;
     for (int t = 0; t < 4; t++) th.emplace_back([c, t] { check_buffer(c, 200000 + 1111 * t, 4096, 900 + t); });
