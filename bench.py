@@ -88,6 +88,27 @@ def cpu_share() -> int:
     return max(1, host_cpu_facts()["share"])
 
 
+# What each workload's parity is pinned by (state it in every parity block).
+PIN_MERKLE = ("reference KAT common/hashtree/hashtree_test.go:20-82 (4 even leaves, each under one block) + NIST "
+              "FIPS 180-4; odd leaf counts, n = 1, multi-block and empty leaves are pinned by two restatements of "
+              "merkletree v0.2.0 only (module not vendored, go.mod:10)")
+PIN_RS = ("klauspost/reedsolomon v1.12.4 TestOneEncode, restated from upstream (module not vendored, go.mod:65); "
+          "everything else restatement-pinned")
+PIN_PROCESS = ("cess-go-sdk FullProcessing composition: parity-unpinned against the SDK (not vendored, go.mod:8); "
+               "its parts are pinned: SHA-256 (NIST), the tree (hashtree_test.go KAT), RS (restated TestOneEncode)")
+PIN_PROOFS = "merkletree v0.2.0 GetMerklePath index rule restated (module not vendored); restatement-pinned"
+
+
+def pinning_for(workload: str, mode: str = "root") -> str:
+    if workload in ("process", "fullprocessing", "process_upload") or (workload == "concurrent" and mode == "process"):
+        return PIN_PROCESS
+    if workload == "rs":
+        return PIN_RS
+    if workload == "proofs":
+        return PIN_PROOFS
+    return PIN_MERKLE
+
+
 def blocks_for(length: int, chunk: int) -> int:
     """Compression blocks of the whole tree: sum ceil((len+9)/64) + 2 x nodes."""
     n = (length + chunk - 1) // chunk
@@ -202,6 +223,8 @@ def main() -> None:
                "process_upload": run_process_upload}
     if args.workload in runners:
         res = runners[args.workload](args, torch, dist, world, rank, device, dev_index, gloo)
+        if isinstance(res, dict) and isinstance(res.get("parity"), dict):
+            res["parity"]["pinned_by"] = pinning_for(args.workload, args.mode)
         if res is not None and rank == 0:
             print(json.dumps(res), flush=True)
         if world > 1 and dist.is_initialized():
@@ -217,6 +240,8 @@ def main() -> None:
         torch.cuda.synchronize()
 
     out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
+    if isinstance(out.get("parity"), dict):
+        out["parity"]["pinned_by"] = PIN_MERKLE
     if world == 1 and rank == 0 and not args.no_extras:
         out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
     if ((world == 8 and not args.same_device) or (world > 1 and args.multi_configs)) and not args.no_extras \
@@ -426,6 +451,7 @@ def multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, b
         ns.total_gib, ns.steps, ns.warmup, ns.no_extras = args.cfg3_total_gib, 3, 1, True
         r = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
         res["configs[3]"] = _summary(r)
+        res["configs[3]"]["pinned_by"] = PIN_MERKLE
     else:
         res["configs[3]"] = {"skipped": f"a rank has less than {need} B of free HBM"}
     res["configs[3]"]["wall_s"] = round(time.perf_counter() - t0, 2)
@@ -434,6 +460,7 @@ def multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, b
     ns = copy.copy(args)
     ns.workload, ns.total_objects, ns.object_mib, ns.steps, ns.warmup = "stream", args.cfg4_objects, 1.0, 2, 1
     res["configs[4]"] = _summary(run_batch(ns, torch, dist, world, rank, device, dev_index, gloo))
+    res["configs[4]"]["pinned_by"] = PIN_MERKLE
     res["configs[4]"]["wall_s"] = round(time.perf_counter() - t0, 2)
     torch.cuda.empty_cache()
     barrier()
@@ -513,6 +540,7 @@ def driver_extras(args, torch, dist, device, dev_index):
         t0 = time.perf_counter()
         try:
             r = _summary(fn(ns, torch, dist, 1, 0, device, dev_index, False))
+            r["pinned_by"] = pinning_for(ns.workload, getattr(ns, "mode", "root"))
         except Exception as e:   # reported, never fatal to the headline line
             r = {"error": f"{type(e).__name__}: {e}"}
         r["wall_s"] = round(time.perf_counter() - t0, 2)
