@@ -65,9 +65,11 @@ def default_context() -> MerkleContext:
 # NewHashTreeFromBuffer objects up to BATCH_LIMIT bytes go through a process-wide coalescing
 # dm_batcher per chunk size, as the Go package does (go/hashtree/types_hip.go): concurrent callers
 # share GPU passes instead of queueing one chain-latency pass each.  Larger
-# objects take dm_root_buffer on the default context (ramped striped H2D, zero-copy when pinned,
-# sharded over its GPUs).
+# objects take dm_root_buffer on the default context (ramped striped H2D, zero-copy when pinned, on
+# its least-loaded GPU).  Only the first MAX_BATCHERS chunk sizes get a batcher (each holds worker
+# contexts on every GPU); other sizes take dm_root_buffer too -- the bound of go/hashtree.
 BATCH_LIMIT = 256 << 20
+MAX_BATCHERS = 4
 _batchers: dict = {}
 _batch_lock = None
 
@@ -79,6 +81,8 @@ def _batcher(chunk: int):
         _batch_lock = threading.Lock()
     with _batch_lock:
         b = _batchers.get(chunk)
+        if b is None and len(_batchers) >= MAX_BATCHERS:
+            return None
         if b is None:
             import atexit
             from .batcher import ROOT, Batcher
@@ -245,8 +249,9 @@ def NewHashTreeFromBuffer(buf: bytes, chunkSize: int, ctx: Optional[MerkleContex
         return None, DeossMerkleError(-1, "Empty data")
     c = ctx or default_context()
     try:
-        if ctx is None and len(buf) <= BATCH_LIMIT:
-            leaves, root = _batcher(chunkSize).root(buf, want_leaves=True)
+        b = _batcher(chunkSize) if ctx is None and len(buf) <= BATCH_LIMIT else None
+        if b is not None:
+            leaves, root = b.root(buf, want_leaves=True)
         else:
             leaves, root = c.root_buffer(buf, chunkSize, want_leaves=True)
     except DeossMerkleError as e:

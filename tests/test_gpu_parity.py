@@ -774,3 +774,17 @@ def test_from_buffer_concurrent_batcher(oracle_lib):
         assert tree.MerkleRoot() == want, g
         assert [n.Hash for n in tree.Leafs[:len(lw)]] == lw, g
     assert _batcher(1 << 20).stats()[0] >= len(bodies)
+
+
+def test_from_buffer_batcher_bound(oracle_lib):
+    """Only the first MAX_BATCHERS chunk sizes get a batcher (each holds worker contexts on every
+    GPU); further sizes take dm_root_buffer -- same trees either way (the go/hashtree bound)."""
+    from deoss_amd import NewHashTreeFromBuffer
+    from deoss_amd import hashtree as ht
+    body = oracle_lib.splitmix_bytes((2 << 20) + 77, 4242)
+    for c in range(1, ht.MAX_BATCHERS + 4):
+        chunk = c << 15
+        tree, err = NewHashTreeFromBuffer(body, chunk)
+        assert err is None
+        assert tree.MerkleRoot() == py_root_chunks(split_chunks(body, chunk))[1], chunk
+    assert len(ht._batchers) <= ht.MAX_BATCHERS
