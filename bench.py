@@ -13,6 +13,7 @@ a chunk-size sweep and the host-buffer end-to-end rate.
 from __future__ import annotations
 
 import argparse
+import gc
 import hashlib
 import json
 import os
@@ -550,6 +551,7 @@ def driver_extras(args, torch, dist, device, dev_index):
             r = {"error": f"{type(e).__name__}: {e}"}
         r["wall_s"] = round(time.perf_counter() - t0, 2)
         res[name] = r
+        gc.collect()   # the workload's contexts and buffers go now, not during the next one's timing
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
     return res
