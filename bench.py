@@ -1616,6 +1616,44 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
     return out if rank == 0 else None
 
 
+def concurrent_callers(ctx, host, length, chunk, root_hex, one_s, dev_index):
+    """T threads each hash the same pinned object through dm_root_buffer at once (T concurrent
+    uploads on one GPU): on the bench's context (DEOSS_LANES call lanes per GPU, default 2) and on a
+    one-lane context (every call serialised on the GPU's one lane)."""
+    import threading
+    from deoss_amd import MerkleContext
+
+    def run(c, T):
+        roots = [None] * T
+        go = threading.Barrier(T + 1)
+
+        def work(i):
+            go.wait()
+            roots[i] = c.root_buffer_ptr(host.data_ptr(), length, chunk)[1].hex()
+
+        th = [threading.Thread(target=work, args=(i,)) for i in range(T)]
+        for t in th:
+            t.start()
+        go.wait()
+        t0 = time.perf_counter()
+        for t in th:
+            t.join()
+        return time.perf_counter() - t0, all(r == root_hex for r in roots)
+
+    res, ok = {"lanes": ctx.lane_count, "one_call_s": round(one_s, 4)}, True
+    for T in (2, 4):
+        s, good = run(ctx, T)
+        ok &= good
+        res[f"threads_{T}"] = {"wall_s": round(s, 4), "GiBps": round(T * length / s / (1 << 30), 4)}
+    with MerkleContext(devices=[dev_index], lanes=1) as one:
+        one.root_buffer_ptr(host.data_ptr(), min(length, 64 << 20), chunk)
+        s, good = run(one, 2)
+        ok &= good
+        res["one_lane_threads_2"] = {"wall_s": round(s, 4), "GiBps": round(2 * length / s / (1 << 30), 4)}
+    res["roots_match"] = ok
+    return res
+
+
 def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -1681,9 +1719,11 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         _, r2 = ctx.root_buffer_ptr(pageable.data_ptr(), length, chunk)
         t3 = time.perf_counter()
         del pageable
+        conc = concurrent_callers(ctx, host, length, chunk, root_hex, t1 - t0, buf.device.index or 0)
         out["e2e"] = {"pinned_host_gibs": round(length / (t1 - t0) / (1 << 30), 4),
                       "pageable_host_gibs": round(length / (t3 - t2) / (1 << 30), 4),
-                      "root_matches": r.hex() == root_hex and r2.hex() == root_hex,
+                      "concurrent_callers": conc,
+                      "root_matches": r.hex() == root_hex and r2.hex() == root_hex and conc["roots_match"],
                       "path": "dm_root_buffer: pinned host memory hashed in place by K1Q over PCIe (zero-copy); "
                               "pageable memory through the pinned ring, H2D striped and overlapped with the leaf "
                               "kernel; tree; 32 B root back"}

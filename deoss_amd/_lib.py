@@ -26,7 +26,8 @@ DM_ERR_NODEV = -7
 
 # Every symbol include/deoss_merkle.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
-    "dm_create", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count", "dm_gpu_count",
+    "dm_create", "dm_create_lanes", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count",
+    "dm_lane_count", "dm_gpu_count",
     "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
     "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
     "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_read_probe_async", "dm_host_alloc",
@@ -62,6 +63,8 @@ def _declare(L: ctypes.CDLL) -> None:
     pvp, pu64 = ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)
     sigs = {
         "dm_create": ([ctypes.POINTER(vp), ctypes.POINTER(i32), i32], i32),
+        "dm_create_lanes": ([ctypes.POINTER(vp), ctypes.POINTER(i32), i32, i32], i32),
+        "dm_lane_count": ([vp], i32),
         "dm_destroy": ([vp], None),
         "dm_strerror": ([i32], ctypes.c_char_p),
         "dm_last_error": ([vp], ctypes.c_char_p),

@@ -218,7 +218,7 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
     const int ns = per * (int)dl.size();
     for (int i = 0; i < ns; i++) {   // slot i on device dl[i % ndev]: consecutive slots alternate GPUs
         dm_ctx* c = nullptr;
-        int rc = dm_create(&c, &dl[i % dl.size()], 1);
+        int rc = dm_create_lanes(&c, &dl[i % dl.size()], 1, 1);   // the slots are the batcher's lanes
         if (rc != DM_OK) {
             t_batcher_err = std::string("dm_batcher_create: ") + dm_strerror(rc);
             dm_batcher_destroy(b);

@@ -293,7 +293,7 @@ int dm_new_hash_tree(dm_ctx* ctx, const char* const* paths, uint64_t n, uint8_t*
         return multi_root(c, G, n, produce, leaf_out, root);
     }
     const int g = pick_device(c);
-    CallLock lk(c, g);
+    CallLock lk(c, g, kReserved);
     Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
     RC_TRY(files_leaves(c, d, fs, 0, n));

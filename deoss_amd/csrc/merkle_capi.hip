@@ -41,6 +41,7 @@ namespace {
 constexpr uint64_t kAlign = 256;                    // leaf start alignment when packing chunks
 constexpr uint64_t kStageBytes = 64ull << 20;       // pinned staging slot
 constexpr uint64_t kStripeBudget = 256ull << 20;    // bytes per H2D stripe / batch (e2e path)
+constexpr int kMaxLanes = 8;                        // call lanes per GPU (dm_create_lanes)
 
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
@@ -217,9 +218,16 @@ struct DevSlot {
 };
 
 struct dm_ctx {
+    // Call lanes: devs holds `lanes` entries per GPU, lane-major (devs[l * nphys + p] is lane l of
+    // GPU p), each with its own streams, scratch and lock, so up to `lanes` calls run on one GPU at
+    // once (an 8 GiB object at 32 MiB chunks keeps 32 of 256 CUs busy for its whole chain).  Lane 0
+    // of every GPU comes first, so a sharded call over G' GPUs locks and uses devs [0, G').
     std::vector<Dev> devs;
-    std::unique_ptr<DevSlot[]> slots;      // one per device (absent in private error-sink contexts)
+    int nphys = 1;                         // GPUs (distinct devices) of the context
+    int lanes = 1;                         // call lanes per GPU (DEOSS_LANES, dm_create_lanes)
+    std::unique_ptr<DevSlot[]> slots;      // one per lane (absent in private error-sink contexts)
     std::atomic<uint32_t> rr{0};           // round-robin start of the least-busy scan
+    std::mutex route_mu;                   // a lane choice and its reservation are one step
     std::mutex comm_mu;
     std::map<int, std::vector<ncclComm_t>> comms;   // RCCL communicators over devices [0, G'), by G'
     std::mutex err_mu;
@@ -310,12 +318,13 @@ struct DeviceRestore {
 // An entry point's hold on ONE device of its context for the whole call (that device's scratch,
 // streams and staging), and the caller's device restored after.  Calls on different devices of one
 // context run concurrently; a thread holds at most one CallLock.
+constexpr bool kReserved = true;   // CallLock on a lane that pick_device / device_of already counted
 struct CallLock {
     DeviceRestore dev;
     DevSlot* slot;
     std::unique_lock<std::mutex> lk;
-    CallLock(dm_ctx* c, int g) : slot(&c->slots[g]) {
-        slot->load++;
+    CallLock(dm_ctx* c, int g, bool reserved = false) : slot(&c->slots[g]) {
+        if (!reserved) slot->load++;
         lk = std::unique_lock<std::mutex>(slot->mu);
     }
     ~CallLock() {
@@ -346,21 +355,43 @@ struct RangeLock {
     RangeLock& operator=(const RangeLock&) = delete;
 };
 
-// Device for a call that can run anywhere: the least-loaded one, ties broken round-robin.
-int pick_device(dm_ctx* c) {
-    const int G = (int)c->devs.size();
-    if (G <= 1) return 0;
-    const int start = (int)(c->rr.fetch_add(1) % (uint32_t)G);
-    int best = start, best_load = c->slots[start].load.load();
-    for (int i = 1; i < G; i++) {
-        const int g = (start + i) % G;
-        const int l = c->slots[g].load.load();
-        if (l < best_load) {
-            best = g;
-            best_load = l;
+// Lane for a call that can run anywhere, counted in its load before return (the caller's
+// CallLock(..., kReserved) or stream releases it): the GPU whose lanes carry the least load, ties
+// broken round-robin, then that GPU's least-loaded lane (lower lanes first).  Choice and count
+// happen under route_mu, so concurrent callers see each other's picks.
+int pick_lane_of(dm_ctx* c, int p) {
+    int best = p, best_load = c->slots[p].load.load();
+    for (int l = 1; l < c->lanes; l++) {
+        const int i = l * c->nphys + p;
+        const int x = c->slots[i].load.load();
+        if (x < best_load) {
+            best = i;
+            best_load = x;
         }
     }
     return best;
+}
+
+int pick_device(dm_ctx* c) {
+    std::lock_guard<std::mutex> lk(c->route_mu);
+    const int P = c->nphys;
+    int bp = 0;
+    if (P > 1) {
+        const int start = (int)(c->rr.fetch_add(1) % (uint32_t)P);
+        int best_load = -1;
+        for (int i = 0; i < P; i++) {
+            const int p = (start + i) % P;
+            int x = 0;
+            for (int l = 0; l < c->lanes; l++) x += c->slots[l * P + p].load.load();
+            if (best_load < 0 || x < best_load) {
+                bp = p;
+                best_load = x;
+            }
+        }
+    }
+    const int g = pick_lane_of(c, bp);
+    c->slots[g].load++;
+    return g;
 }
 
 // Calls already running or queued on the context (routing: a busy context never shards).
@@ -443,19 +474,24 @@ hipError_t pinned_grow(dm_ctx* c, int dev, PinnedBuf& b, uint64_t n) {
     return b.ensure(n);
 }
 
-// Device holding device memory p (device-resident entry points run where their data lives);
-// the first device when p is not device memory of one of the context's devices.
+// Lane for a device-memory call (device-resident entry points run where their data lives), counted
+// like pick_device: the least-loaded lane of the GPU holding p, or of the first GPU when p is not
+// device memory of one of the context's GPUs.
 int device_of(dm_ctx* c, const void* p) {
-    if (c->devs.size() <= 1 || !p) return 0;
-    hipPointerAttribute_t attr{};
-    int g = 0;
-    if (hipPointerGetAttributes(&attr, p) == hipSuccess)
-        for (size_t i = 0; i < c->devs.size(); i++)
-            if (c->devs[i].id == attr.device) {
-                g = (int)i;
-                break;
-            }
-    (void)hipGetLastError();
+    int phys = 0;
+    if (c->nphys > 1 && p) {
+        hipPointerAttribute_t attr{};
+        if (hipPointerGetAttributes(&attr, p) == hipSuccess)
+            for (int i = 0; i < c->nphys; i++)
+                if (c->devs[i].id == attr.device) {
+                    phys = i;
+                    break;
+                }
+        (void)hipGetLastError();
+    }
+    std::lock_guard<std::mutex> lk(c->route_mu);
+    const int g = pick_lane_of(c, phys);
+    c->slots[g].load++;
     return g;
 }
 
@@ -1173,7 +1209,7 @@ int host_src(const void* p) {
 
 // Devices a host-memory call uses (dm_plan::route; forced sharding is a test hook).
 int route_call(dm_ctx* c, uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, bool by_objects = false) {
-    const int G = (int)c->devs.size();
+    const int G = c->nphys;   // GPUs; a call never shards over lanes of one GPU
     if (c->force_sharded) return n >= 2 * (uint64_t)G ? G : 1;
     if (G <= 1) return 1;
     return dm_plan::route(n, bytes, leaf_max, src, G, c->devs[0].cus, c->leaf_mode.load(), ctx_load(c), by_objects);
@@ -1182,7 +1218,7 @@ int route_call(dm_ctx* c, uint64_t n, uint64_t bytes, uint64_t leaf_max, int src
 // Whether a call of n leaves routed to G devices takes the multi-device path (with
 // DEOSS_FORCE_SHARDED even G = 1 does, when n >= 2 x the context's devices).
 bool sharded(const dm_ctx* c, int G, uint64_t n) {
-    return G > 1 || (c->force_sharded && n >= 2 * (uint64_t)c->devs.size());
+    return G > 1 || (c->force_sharded && n >= 2 * (uint64_t)c->nphys);
 }
 
 // Leaf digests of host chunks into d.leaves (stream-ordered on d.stream): read in place from
@@ -1279,7 +1315,9 @@ const char* dm_strerror(int rc) {
 
 const char* dm_last_error(dm_ctx*) { return t_err.c_str(); }
 
-int dm_device_count(dm_ctx* ctx) { return ctx ? (int)ctx->devs.size() : 0; }
+int dm_device_count(dm_ctx* ctx) { return ctx ? ctx->nphys : 0; }
+
+int dm_lane_count(dm_ctx* ctx) { return ctx ? ctx->lanes : 0; }
 
 int dm_gpu_count(void) {
     int n = 0;
@@ -1307,8 +1345,23 @@ void dm_host_free(void* p) {
     if (p) (void)hipHostFree(p);
 }
 
-int dm_create(dm_ctx** out, const int* devs, int ndev) {
-    if (!out) return bad_arg();
+}  // extern "C"
+
+namespace {
+
+// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else 2.  Two lanes let
+// two large calls share a GPU (measured 2x for concurrent 8 GiB objects, tools/lanes_probe.py,
+// profiles/r03/r03m_lanes.log); more gained nothing there, because a process's streams share
+// GPU_MAX_HW_QUEUES (4) hardware queues and a kernel waits behind any other kernel on its queue
+// (tools/hwq_probe.hip).
+int default_lanes() {
+    const char* v = std::getenv("DEOSS_LANES");
+    const int n = v ? std::atoi(v) : 2;
+    return std::min(std::max(n, 1), kMaxLanes);
+}
+
+int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
+    if (!out || lanes < 1 || lanes > kMaxLanes) return bad_arg();
     *out = nullptr;
     DeviceRestore dev;
     int count = 0;
@@ -1323,12 +1376,17 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     }
     const char* vd = std::getenv("DEOSS_VIRTUAL_DEVICES");   // test hook (dm_ctx::virtual_devs)
     const int nvirt = vd ? std::atoi(vd) : 0;
-    if (nvirt > 1) ids.assign((size_t)std::min(nvirt, 64), ids[0]);
+    if (nvirt > 1) {
+        ids.assign((size_t)std::min(nvirt, 64), ids[0]);
+        lanes = 1;   // every virtual device stands for a GPU of its own
+    }
     dm_ctx* c = new dm_ctx();
-    c->devs.resize(ids.size());
-    c->slots.reset(new DevSlot[ids.size()]);
-    for (size_t i = 0; i < ids.size(); i++) {
-        c->devs[i].id = ids[i];
+    c->nphys = (int)ids.size();
+    c->lanes = lanes;
+    c->devs.resize(ids.size() * (size_t)lanes);
+    c->slots.reset(new DevSlot[c->devs.size()]);
+    for (size_t i = 0; i < c->devs.size(); i++) {   // lane-major: lane 0 of every GPU first
+        c->devs[i].id = ids[i % ids.size()];
         int rc = init_device(c, c->devs[i]);
         if (rc != DM_OK) {
             dm_destroy(c);
@@ -1349,6 +1407,14 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     *out = c;
     return DM_OK;
 }
+
+}  // namespace
+
+extern "C" {
+
+int dm_create(dm_ctx** out, const int* devs, int ndev) { return ctx_create(out, devs, ndev, default_lanes()); }
+
+int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) { return ctx_create(out, devs, ndev, lanes); }
 
 void dm_destroy(dm_ctx* ctx) {
     if (!ctx) return;
@@ -1437,7 +1503,7 @@ int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t ch
                          void* leaf_out_dev, void* stream) {
     if (!ctx || !dev_root || chunk == 0 || (!dev && len)) return bad_arg();
     const int g = device_of(ctx, dev);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     Dev& d = ctx->devs[g];
     return root_device_impl(ctx, d, pick_stream(d, stream), dev, len, chunk, static_cast<uint8_t*>(dev_root),
                             static_cast<uint8_t*>(leaf_out_dev));
@@ -1446,7 +1512,7 @@ int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t ch
 int dm_root_device(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, uint8_t root[32]) {
     if (!ctx || !root || chunk == 0 || (!dev && len)) return bad_arg();
     const int g = device_of(ctx, dev);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     Dev& d = c->devs[g];
     RC_TRY(root_device_impl(c, d, d.stream, dev, len, chunk, d.root.u8(), nullptr));
@@ -1459,7 +1525,7 @@ int dm_subtree_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t
                             void* dev_nodes, uint64_t* n_out, void* stream) {
     if (!ctx || !dev_nodes || chunk == 0 || (!dev && len) || levels > 63) return bad_arg();
     const int g = device_of(ctx, dev);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[g];
@@ -1477,7 +1543,7 @@ int dm_finish_device_async(dm_ctx* ctx, const void* dev_nodes, uint64_t n, int m
                            void* stream) {
     if (!ctx || !dev_nodes || !dev_root) return bad_arg();
     const int g = device_of(ctx, dev_nodes);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[g];
@@ -1491,7 +1557,7 @@ int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const u
                                uint64_t chunk, void* dev_roots, void* stream) {
     if (!ctx || chunk == 0 || (nobj && (!dev_objs || !lens || !dev_roots))) return bad_arg();
     const int g = device_of(ctx, dev_roots);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (nobj == 0) return DM_OK;
     Dev& d = c->devs[g];
@@ -1503,7 +1569,7 @@ int dm_root_batch_device_async(dm_ctx* ctx, const void* const* dev_objs, const u
 int dm_fill_synthetic_async(dm_ctx* ctx, void* dev, uint64_t off, uint64_t nbytes, uint64_t seed, void* stream) {
     if (!ctx || (!dev && nbytes) || off % 8 || nbytes % 8 || !is_aligned16(dev)) return bad_arg();
     const int g = device_of(ctx, dev);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (nbytes == 0) return DM_OK;
     Dev& d = c->devs[g];
@@ -1522,7 +1588,7 @@ int dm_read_probe_async(dm_ctx* ctx, const void* dev, uint64_t nbytes, void* dev
         reinterpret_cast<uintptr_t>(dev_xor8) % 8)
         return bad_arg();
     const int g = device_of(ctx, dev_xor8);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
@@ -1553,7 +1619,7 @@ int dm_root_buffer(dm_ctx* ctx, const void* host, uint64_t len, uint64_t chunk, 
         return root_buffer_multi(c, G, host, len, chunk, leaf_out, root);
     }
     const int g = pick_device(c);
-    CallLock lk(c, g);
+    CallLock lk(c, g, kReserved);
     Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
     RC_TRY(h2d_and_hash_leaves(c, d, host, len, chunk));
@@ -1581,7 +1647,7 @@ int dm_root_chunks(dm_ctx* ctx, const void* const* ptrs, const uint64_t* lens, u
         return multi_root(c, G, n, produce, leaf_out, root);
     }
     const int g = pick_device(c);
-    CallLock lk(c, g);
+    CallLock lk(c, g, kReserved);
     Dev& d = c->devs[g];
     RC_TRY(begin_call(c, d, d.stream));
     RC_TRY(chunks_leaves(c, d, ptrs, lens, n));
@@ -1609,7 +1675,7 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
         return batch_host_multi(c, G, objs, lens, nobj, chunk, roots);
     }
     const int g = pick_device(c);
-    CallLock lk(c, g);
+    CallLock lk(c, g, kReserved);
     return batch_host_on(c, c->devs[g], objs, lens, nobj, chunk, roots);
 }
 

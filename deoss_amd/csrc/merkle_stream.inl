@@ -199,10 +199,9 @@ int dm_stream_open(dm_ctx* ctx, uint64_t chunk, dm_stream** out) {
     if (chunk % 16 != 0) return fail(ctx, DM_ERR_INVALID, "dm_stream: chunk must be a multiple of 16 bytes");
     dm_stream* st = new dm_stream();
     st->c = ctx;
-    // a stream keeps one device busy while the body arrives: the least-loaded one, counted in its
-    // load until the stream is freed, so concurrent uploads spread over the context's devices
+    // a stream keeps one lane busy while the body arrives: the least-loaded one, counted in its
+    // load until the stream is freed, so concurrent uploads spread over the context's GPUs and lanes
     st->dev = pick_device(ctx);
-    ctx->slots[st->dev].load++;
     st->tree.id = ctx->devs[st->dev].id;
     st->tree.cus = ctx->devs[st->dev].cus;
     st->chunk = chunk;

@@ -117,7 +117,7 @@ uint32_t dm_tree_depth(uint64_t n) { return tree_depth(n); }
 int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n, void* dev_nodes, void* stream) {
     if (!ctx) return bad_arg();
     const int g = device_of(ctx, dev_nodes);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (!aligned_all({dev_leaves, dev_nodes}))
@@ -131,7 +131,7 @@ int dm_tree_levels_device_async(dm_ctx* ctx, const void* dev_leaves, uint64_t n,
 int dm_tree_levels(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, uint8_t* nodes_out) {
     if (!ctx || (n && (!leaf_digests || !nodes_out))) return bad_arg();
     const int g = pick_device(ctx);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     Dev& d = c->devs[g];
@@ -151,7 +151,7 @@ int dm_merkle_paths_device_async(dm_ctx* ctx, const void* dev_leaves, const void
                                  const void* dev_idx, uint64_t q, void* dev_paths, void* dev_bits, void* stream) {
     if (!ctx) return bad_arg();
     const int g = device_of(ctx, dev_paths);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
@@ -170,7 +170,7 @@ int dm_merkle_paths(dm_ctx* ctx, const uint8_t* leaf_digests, uint64_t n, const 
                     uint8_t* paths, uint8_t* bits) {
     if (!ctx || (n && !leaf_digests) || (q && (!idx || !paths || !bits))) return bad_arg();
     const int g = pick_device(ctx);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (n == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (q == 0) return DM_OK;
@@ -200,7 +200,7 @@ int dm_verify_paths_device_async(dm_ctx* ctx, const void* const* dev_contents, c
                                  uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
     const int g = device_of(ctx, dev_ok);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     if (!dev_contents || !lens || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
@@ -222,7 +222,7 @@ int dm_verify_object_device_async(dm_ctx* ctx, const void* dev_obj, uint64_t len
                                   uint64_t root_stride, void* dev_ok, void* stream) {
     if (!ctx) return bad_arg();
     const int g = device_of(ctx, dev_obj);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (len == 0) return fail(c, DM_ERR_EMPTY, "Empty data");
     if (chunk == 0 || !dev_obj || !dev_bits || !dev_ok || depth == 0 || !aligned_all({dev_paths, dev_roots}) ||
@@ -242,7 +242,7 @@ int dm_verify_paths(dm_ctx* ctx, const void* const* contents, const uint64_t* le
         (root_stride != 0 && root_stride != 32))
         return bad_arg();
     const int g = pick_device(ctx);
-    CallLock lk(ctx, g);
+    CallLock lk(ctx, g, kReserved);
     dm_ctx* c = ctx;
     if (q == 0) return DM_OK;
     for (uint64_t t = 0; t < q; t++)

@@ -17,14 +17,16 @@ from ._lib import DM_ERR_EMPTY, DeossMerkleError, load_library
 
 
 class MerkleContext:
-    def __init__(self, devices: Optional[Sequence[int]] = None):
+    def __init__(self, devices: Optional[Sequence[int]] = None, lanes: Optional[int] = None):
+        """``lanes``: call lanes per GPU (``dm_create_lanes``); None = ``DEOSS_LANES`` or 2."""
         self._L = load_library()
         h = ctypes.c_void_p()
-        if devices:
-            arr = (ctypes.c_int * len(devices))(*devices)
-            rc = self._L.dm_create(ctypes.byref(h), arr, len(devices))
+        arr = (ctypes.c_int * len(devices))(*devices) if devices else None
+        n = len(devices) if devices else 0
+        if lanes is None:
+            rc = self._L.dm_create(ctypes.byref(h), arr, n)
         else:
-            rc = self._L.dm_create(ctypes.byref(h), None, 0)
+            rc = self._L.dm_create_lanes(ctypes.byref(h), arr, n, int(lanes))
         if rc != 0:
             raise DeossMerkleError(rc, f"dm_create: {self._L.dm_strerror(rc).decode()}")
         self._h = h
@@ -54,6 +56,10 @@ class MerkleContext:
     @property
     def device_count(self) -> int:
         return self._L.dm_device_count(self._h)
+
+    @property
+    def lane_count(self) -> int:
+        return self._L.dm_lane_count(self._h)
 
     def _check(self, rc: int, what: str) -> None:
         if rc == 0:

@@ -60,12 +60,18 @@ enum {
  * With ndev > 1, each host-memory call runs whole on the least-loaded device, unless dm_plan_route
  * shards it: a single object is then split by aligned chunk ranges across devices [0, G') and the
  * per-device subtree roots are gathered with RCCL ("C1"); a batch is split by
- * objects with no exchange. */
+ * objects with no exchange.
+ * Every GPU carries DEOSS_LANES (default 2, at most 8) call lanes: each lane has its own streams,
+ * scratch and lock, so that many calls run on one GPU at once and concurrent callers (one gin
+ * goroutine per upload) are not serialised behind each other's leaf chains. */
 int dm_create(dm_ctx **out, const int *devs, int ndev);
+/* dm_create with an explicit lane count per GPU (1..8). */
+int dm_create_lanes(dm_ctx **out, const int *devs, int ndev, int lanes);
 void dm_destroy(dm_ctx *ctx);
 const char *dm_strerror(int rc);
 const char *dm_last_error(dm_ctx *ctx);   /* ctx is ignored (kept for ABI compatibility) */
-int dm_device_count(dm_ctx *ctx);
+int dm_device_count(dm_ctx *ctx);         /* GPUs of the context */
+int dm_lane_count(dm_ctx *ctx);           /* call lanes per GPU */
 /* GPUs visible to this process (HIP device count; 0 without a usable GPU).  Lets a binding
  * default to every GPU of the node: dm_create(ctx, {0 .. dm_gpu_count()-1}, n). */
 int dm_gpu_count(void);

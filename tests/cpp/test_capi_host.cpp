@@ -168,6 +168,34 @@ static void go_stream_sequence(dm_ctx* c, uint64_t len, uint64_t chunk, uint64_t
     EXPECT(got == n && std::memcmp(rw, rg, 32) == 0 && lw == lg);
 }
 
+// One thread's mix of host-memory calls (buffers, streams -- some aborted --, batches), each
+// checked against the oracle: the concurrent-routing workload of the multi-device / lanes blocks.
+static void mixed_calls(dm_ctx* cv, int t) {
+    for (int i = 0; i < 3; i++) {
+        switch ((t + i) % 3) {
+            case 0: check_buffer(cv, 150000 + 4099 * (3 * t + i), 8192, 1300 + 3 * t + i); break;
+            case 1: go_stream_sequence(cv, 2000000 + 777 * t, 65536, 1400 + t, (t + i) % 5 == 0); break;
+            default: {
+                std::vector<std::vector<uint8_t>> objs;
+                for (int o = 0; o < 5; o++) objs.push_back(bytes(30000 + 1000 * o + t, 1500 + 10 * t + o));
+                std::vector<const void*> op;
+                std::vector<uint64_t> ol;
+                for (auto& o : objs) {
+                    op.push_back(o.data());
+                    ol.push_back(o.size());
+                }
+                std::vector<uint8_t> roots(32 * objs.size());
+                EXPECT(dm_root_batch(cv, op.data(), ol.data(), objs.size(), 4096, roots.data()) == DM_OK);
+                for (size_t o = 0; o < objs.size(); o++) {
+                    uint8_t r[32];
+                    EXPECT(or_root_buffer(objs[o].data(), objs[o].size(), 4096, nullptr, r, 1) == 0);
+                    EXPECT(std::memcmp(r, roots.data() + 32 * o, 32) == 0);
+                }
+            }
+        }
+    }
+}
+
 int main(int argc, char** argv) {
     const std::string tmpdir = argc > 1 ? argv[1] : "/tmp";
     dm_ctx* c = nullptr;
@@ -633,32 +661,7 @@ int main(int argc, char** argv) {
         if (cv && cvs) {
             EXPECT(dm_device_count(cv) == 4);
             std::vector<std::thread> vt;
-            for (int t = 0; t < 8; t++)
-                vt.emplace_back([cv, t] {
-                    for (int i = 0; i < 3; i++) {
-                        switch ((t + i) % 3) {
-                            case 0: check_buffer(cv, 150000 + 4099 * (3 * t + i), 8192, 1300 + 3 * t + i); break;
-                            case 1: go_stream_sequence(cv, 2000000 + 777 * t, 65536, 1400 + t, (t + i) % 5 == 0); break;
-                            default: {
-                                std::vector<std::vector<uint8_t>> objs;
-                                for (int o = 0; o < 5; o++) objs.push_back(bytes(30000 + 1000 * o + t, 1500 + 10 * t + o));
-                                std::vector<const void*> op;
-                                std::vector<uint64_t> ol;
-                                for (auto& o : objs) {
-                                    op.push_back(o.data());
-                                    ol.push_back(o.size());
-                                }
-                                std::vector<uint8_t> roots(32 * objs.size());
-                                EXPECT(dm_root_batch(cv, op.data(), ol.data(), objs.size(), 4096, roots.data()) == DM_OK);
-                                for (size_t o = 0; o < objs.size(); o++) {
-                                    uint8_t r[32];
-                                    EXPECT(or_root_buffer(objs[o].data(), objs[o].size(), 4096, nullptr, r, 1) == 0);
-                                    EXPECT(std::memcmp(r, roots.data() + 32 * o, 32) == 0);
-                                }
-                            }
-                        }
-                    }
-                });
+            for (int t = 0; t < 8; t++) vt.emplace_back([cv, t] { mixed_calls(cv, t); });
             for (auto& x : vt) x.join();
             for (auto [len, chunk] : {std::pair<uint64_t, uint64_t>{777ull * 4096 + 5, 4096}, {(100ull << 20) + 3, 8ull << 20}}) {
                 auto b = bytes(len, len + 5);
@@ -672,6 +675,22 @@ int main(int argc, char** argv) {
         }
         dm_destroy(cv);
         dm_destroy(cvs);
+    }
+
+    // call lanes (dm_create_lanes): four lanes of this GPU, each with its own streams, scratch and
+    // lock, under the same 8-thread mix; bad lane counts are rejected
+    {
+        dm_ctx* cl = nullptr;
+        EXPECT(dm_create_lanes(&cl, nullptr, 0, 0) == DM_ERR_INVALID && cl == nullptr);
+        EXPECT(dm_create_lanes(&cl, nullptr, 0, 9) == DM_ERR_INVALID && cl == nullptr);
+        EXPECT(dm_create_lanes(&cl, nullptr, 0, 4) == DM_OK);
+        if (cl) {
+            EXPECT(dm_device_count(cl) == 1 && dm_lane_count(cl) == 4);
+            std::vector<std::thread> lt;
+            for (int t = 0; t < 8; t++) lt.emplace_back([cl, t] { mixed_calls(cl, t); });
+            for (auto& x : lt) x.join();
+        }
+        dm_destroy(cl);
     }
 
     // concurrent callers on one context

@@ -521,6 +521,76 @@ def test_virtual_devices_concurrent_routing(oracle_lib):
         c.close()
 
 
+def test_lanes_concurrent_calls(oracle_lib, tmp_path):
+    """Call lanes (dm_create_lanes): 4 lanes of this box's one GPU, each with its own streams,
+    scratch and lock.  16 threads mix host buffers (pinned zero-copy and pageable), chunk lists,
+    streams, batches, files and device-resident calls on their own torch streams; every root
+    matches the oracle.  A sharded-forced context keeps lane 0 for its sharded calls."""
+    import threading
+    from deoss_amd import MerkleContext
+    torch = _torch()
+    c = MerkleContext(lanes=4)
+    assert (c.device_count, c.lane_count) == (1, 4)
+    datas = [oracle_lib.splitmix_bytes(20000 + 37 * i, 1900 + i) for i in range(12)]
+    paths = _write_files(tmp_path, datas, "lane_")
+    files_want = oracle_lib.root_chunks(datas, nthreads=8)
+    errors = []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            for i in range(3):
+                data = oracle_lib.splitmix_bytes(150000 + 7919 * (3 * t + i), 9000 + 3 * t + i)
+                want = oracle_lib.root_buffer(data, 8192)[1]
+                kind = (t + i) % 6
+                if kind == 0:
+                    got = c.root_buffer(data, 8192, want_leaves=False)[1]
+                elif kind == 1:
+                    pin = torch.frombuffer(bytearray(data), dtype=torch.uint8).pin_memory()
+                    got = c.root_buffer_ptr(pin.data_ptr(), len(data), 8192)[1]
+                elif kind == 2:
+                    got = c.root_chunks([data[o:o + 8192] for o in range(0, len(data), 8192)])[1]
+                elif kind == 3:
+                    st = c.open_stream(8192)
+                    st.write(data[:5000])
+                    st.write(data[5000:])
+                    got = st.close()[1]
+                elif kind == 4:
+                    got = c.root_batch([data, data[:3000]], 8192)[0]
+                else:
+                    with torch.cuda.stream(s):
+                        dv = torch.frombuffer(bytearray(data), dtype=torch.uint8).to("cuda", non_blocking=False)
+                        r = torch.zeros(32, dtype=torch.uint8, device="cuda")
+                        c.root_device_async(dv.data_ptr(), len(data), 8192, r.data_ptr(), 0, s.cuda_stream)
+                    s.synchronize()
+                    got = bytes(r.cpu().numpy())
+                if got != want:
+                    errors.append((t, i, kind))
+            leaves, root = c.new_hash_tree(paths)
+            if (b"".join(leaves), root) != files_want:
+                errors.append((t, "files"))
+        except Exception as e:   # reported below
+            errors.append((t, repr(e)))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert errors == []
+    finally:
+        c.close()
+    s = _forced_sharded_context()
+    try:
+        assert s.lane_count == 2   # dm_create's default
+        host = oracle_lib.splitmix_bytes(1000 * 4096 + 7, 31)
+        lw, want = oracle_lib.root_buffer(host, 4096, nthreads=8)
+        assert s.root_buffer(host, 4096, want_leaves=True) == (lw, want)
+    finally:
+        s.close()
+
+
 def _write_files(tmp_path, datas, tag):
     paths = []
     for i, d in enumerate(datas):

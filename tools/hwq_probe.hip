@@ -7,10 +7,12 @@
 // For every ordered pair (A, B): a 30 ms spin kernel on A, then (10 ms later) a 1-thread kernel
 // on B; B "waits" if its kernel ends after the spin.  Streams: normal, high and low priority, in
 // creation order, then the same after destroying some (what a process with earlier contexts sees).
+// usage: hwq_probe [high-priority streams (3)] [normal streams (8)]
 // Build: hipcc --offload-arch=gfx950 -O2 -o tools/hwq_probe tools/hwq_probe.hip
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -81,7 +83,9 @@ static int matrix(const std::vector<Named>& ss, int* out, void* host, void* dev,
     return 0;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const int nhigh = argc > 1 ? std::atoi(argv[1]) : 3;   // high-priority streams to create
+    const int nnorm = argc > 2 ? std::atoi(argv[2]) : 8;
     int* out = nullptr;
     void* dev = nullptr;
     void* host = nullptr;
@@ -93,12 +97,12 @@ int main() {
     std::printf("priority range: least %d greatest %d; GPU_MAX_HW_QUEUES=%s\n", lo, hi,
                 std::getenv("GPU_MAX_HW_QUEUES") ? std::getenv("GPU_MAX_HW_QUEUES") : "(unset)");
     std::vector<Named> ss;
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < nnorm; i++) {
         hipStream_t s;
         CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         ss.push_back({s, "n" + std::to_string(i)});
     }
-    for (int i = 0; i < 3; i++) {
+    for (int i = 0; i < nhigh; i++) {
         hipStream_t s;
         CK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
         ss.push_back({s, "h" + std::to_string(i)});
