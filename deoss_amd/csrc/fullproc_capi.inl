@@ -242,7 +242,7 @@ int fp_striped_pass(dm_rs* r, Dev& d, hipStream_t s, StreamKit* kit, const FileS
         const uint64_t o = so[j], w = sw[j], q = o / frag;
         int sl;
         RC_TRY(take_slot(&sl));
-        uint8_t* buf = r->fp_slot[sl].u8();
+        uint8_t* buf = rs_ln(r, d).fp_slot[sl].u8();
         std::vector<FilePart> parts;
         for (uint64_t t = 0; t < ns; t++) {
             const uint64_t a = fbeg + t * seg + o;
@@ -305,11 +305,12 @@ int fp_striped_pass(dm_rs* r, Dev& d, hipStream_t s, StreamKit* kit, const FileS
 }
 
 // Everything but the renames; `pend` collects (temporary name, digest slot) of every file written.
-int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir, uint64_t seg, int flags,
+int full_processing_windows(dm_rs* r, Dev& d, const FileSet& fs, const std::string& dir, uint64_t seg, int flags,
                             std::vector<uint8_t>& segd, std::vector<uint8_t>& fragd,
                             std::vector<std::pair<std::string, uint64_t>>& pend, uint8_t fid[32]) {
     dm_ctx* c = r->c;
-    Dev& d = c->devs[0];
+    const int g = (int)(&d - c->devs.data());   // the call's lane
+    RsLane& L = rs_ln(r, d);
     hipStream_t s = d.stream;
     const int k = r->k, m = r->m, total = k + m;
     const uint64_t frag = seg / (uint64_t)k, pbytes = (uint64_t)m * frag;   // parity bytes per segment
@@ -323,7 +324,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
     const uint64_t win = std::max<uint64_t>(spd, window_bytes / seg / spd * spd);   // segments per window
     const int readers = (int)std::min<uint64_t>(64, env_bytes("DEOSS_FP_READERS", kFpReaders));
     RC_TRY(begin_call(c, d, s));
-    for (auto& b : r->fp_slot) HIP_TRY(b.ensure(slot_cap));
+    for (auto& b : L.fp_slot) HIP_TRY(b.ensure(slot_cap));
     FpEvents ev;
     for (auto& e : ev.slot) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&ev.rs, hipEventDisableTiming));
@@ -384,15 +385,16 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
     const bool stripes_off = stripes_env != nullptr && stripes_env[0] == '0';
     // two extra compute streams for the striped pass (segment and data-fragment chains side by side)
     StreamKit* kit = nullptr;
-    RC_TRY(kit_acquire(c, 0, &kit));
+    RC_TRY(kit_acquire(c, g, &kit));
     struct KitBack {
         dm_ctx* c;
+        int g;
         StreamKit* k;
         ~KitBack() {
             for (hipStream_t x : {k->comp[0], k->comp[1]}) (void)hipStreamSynchronize(x);
-            kit_release(c, 0, k);
+            kit_release(c, g, k);
         }
-    } kit_back{c, kit};
+    } kit_back{c, g, kit};
     FpTrace tr;
     for (uint64_t w0 = 0; w0 < nseg; w0 += win) {
         const uint64_t ns = std::min(win, nseg - w0);
@@ -403,8 +405,8 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
         // per fragment.  DEOSS_FP_STRIPES=0 keeps the read-then-launch order (A/B).
         const bool striped = ns >= kFpStripeMinSegs && frag % 64 == 0 && !stripes_off;
         HIP_TRY(d.data.ensure(ns * seg + kAlign));
-        HIP_TRY(r->work.ensure(ns * pbytes + 256 + 2 * ns * 32));
-        uint8_t* parity = r->work.u8();
+        HIP_TRY(L.work.ensure(ns * pbytes + 256 + 2 * ns * 32));
+        uint8_t* parity = L.work.u8();
         uint8_t* dfid = parity + ns * pbytes;
         if (!striped) {
             // A: file -> slots -> HBM, nothing else, so the leaf chains start as early as the reads allow
@@ -412,7 +414,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
                 const uint64_t nt = std::min(spd, ns - t0), len = nt * seg, a = fbeg + t0 * seg;
                 int sl;
                 RC_TRY(take_slot(&sl));
-                uint8_t* buf = r->fp_slot[sl].u8();
+                uint8_t* buf = L.fp_slot[sl].u8();
                 const uint64_t have = a < fend ? std::min(len, fend - a) : 0;
                 std::vector<FilePart> parts;
                 for (uint64_t q = 0; q < have; q += 8ull << 20)
@@ -453,7 +455,7 @@ int full_processing_windows(dm_rs* r, const FileSet& fs, const std::string& dir,
             const uint64_t nt = std::min(spp, ns - t0);
             int sl;
             RC_TRY(take_slot(&sl));
-            uint8_t* buf = r->fp_slot[sl].u8();
+            uint8_t* buf = L.fp_slot[sl].u8();
             HIP_TRY(hipMemcpyAsync(buf, parity + t0 * pbytes, nt * pbytes, hipMemcpyDeviceToHost, d.copy));
             HIP_TRY(hipEventRecord(ev.slot[sl], d.copy));
             HIP_TRY(hipEventSynchronize(ev.slot[sl]));
@@ -521,7 +523,8 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
                        uint8_t* seg_hashes, uint8_t* frag_hashes, uint64_t cap, uint64_t* nseg_out, uint8_t fid[32]) {
     if (!r || !path || !savedir || !fid) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (nseg_out) *nseg_out = 0;
     FileSet fs;
     RC_TRY(open_files(c, &path, 1, fs));   // "open <path>: ..." first, as os.Open would fail
@@ -540,9 +543,9 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
     const int total = r->k + r->m;
     std::vector<uint8_t> segd(32 * nseg), fragd(32 * nseg * total);
     std::vector<std::pair<std::string, uint64_t>> pend;
-    int rc = full_processing_windows(r, fs, dir, segment, flags, segd, fragd, pend, fid);
+    Dev& d = c->devs[g];
+    int rc = full_processing_windows(r, d, fs, dir, segment, flags, segd, fragd, pend, fid);
     {
-        Dev& d = c->devs[0];
         if (rc != DM_OK) {   // a failed call may leave copies queued: none may land in a slot the next call fills
             (void)hipStreamSynchronize(d.copy);
             (void)hipStreamSynchronize(d.stream);
@@ -551,7 +554,7 @@ int dm_full_processing(dm_rs* r, const char* path, const char* savedir, uint64_t
         // back what a large call took beyond kFpKeepBytes, so it does not stay resident beside
         // other work on this GPU; the call has synchronised its streams already
         if (d.data.cap > kFpKeepBytes) c->reaper.put(d.id, d.data);
-        if (r->work.cap > kFpKeepBytes) c->reaper.put(d.id, r->work);
+        if (rs_ln(r, d).work.cap > kFpKeepBytes) c->reaper.put(d.id, rs_ln(r, d).work);
     }
     for (size_t i = 0; rc == DM_OK && i < pend.size(); i++) {
         const uint64_t at = pend[i].second;

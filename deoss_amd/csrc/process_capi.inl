@@ -108,8 +108,9 @@ int process_host(dm_rs* r, Dev& d, const void* const* objs, const uint64_t* lens
         const uint64_t pad = (first[o + 1] - first[o]) * segment - lens[o];
         if (pad) HIP_TRY(hipMemsetAsync(d.data.u8() + off[o] + lens[o], 0, pad, s));
     }
-    HIP_TRY(r->work.ensure(S * (uint64_t)m * frag + nobj * 32));
-    uint8_t* parity = r->work.u8();
+    DevBuf& work = rs_ln(r, d).work;
+    HIP_TRY(work.ensure(S * (uint64_t)m * frag + nobj * 32));
+    uint8_t* parity = work.u8();
     uint8_t* dfid = parity + S * (uint64_t)m * frag;
     RC_TRY(process_segments(r, d, s, d.data.u8(), segment, parity, first, dfid));
     HIP_TRY(hipMemcpyAsync(fids, dfid, nobj * 32, hipMemcpyDeviceToHost, s));
@@ -151,11 +152,12 @@ int dm_process_device_async(dm_rs* r, void* dev_obj, uint64_t len, uint64_t segm
                             void* dev_seg_hashes, void* dev_frag_hashes, void* dev_fid, void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     RC_TRY(process_check(r, len, segment));
     if (!dev_obj || !dev_parity || !dev_fid || !is_aligned16(dev_obj) || !is_aligned16(dev_parity))
         return fail(c, DM_ERR_INVALID, "dm_process_device_async: need 16-byte aligned object and parity buffers");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     return process_dev(r, d, pick_stream(d, stream), static_cast<uint8_t*>(dev_obj), len, segment,
                        static_cast<uint8_t*>(dev_parity), static_cast<uint8_t*>(dev_seg_hashes),
                        static_cast<uint8_t*>(dev_frag_hashes), static_cast<uint8_t*>(dev_fid));
@@ -165,17 +167,19 @@ int dm_process_buffer(dm_rs* r, const void* host, uint64_t len, uint64_t segment
                       uint8_t* seg_hashes, uint8_t* frag_hashes, uint8_t fid[32]) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (!fid || (!host && len)) return fail(c, DM_ERR_INVALID, "dm_process_buffer: null argument");
     RC_TRY(process_check(r, len, segment));
-    return process_host(r, c->devs[0], &host, &len, 1, segment, &frags_out, &seg_hashes, &frag_hashes, fid);
+    return process_host(r, c->devs[g], &host, &len, 1, segment, &frags_out, &seg_hashes, &frag_hashes, fid);
 }
 
 int dm_process_batch(dm_rs* r, const void* const* objs, const uint64_t* lens, uint64_t nobj, uint64_t segment,
                      void* const* frags_out, uint8_t* const* seg_hashes, uint8_t* const* frag_hashes, uint8_t* fids) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (nobj == 0) return DM_OK;
     if (!objs || !lens || !fids) return fail(c, DM_ERR_INVALID, "dm_process_batch: null argument");
     for (uint64_t o = 0; o < nobj; o++) {
@@ -183,7 +187,7 @@ int dm_process_batch(dm_rs* r, const void* const* objs, const uint64_t* lens, ui
         if (!objs[o]) return fail(c, DM_ERR_INVALID, "object %llu: NULL pointer", (unsigned long long)o);
     }
     RC_TRY(process_check(r, lens[0], segment));
-    return process_host(r, c->devs[0], objs, lens, nobj, segment, frags_out, seg_hashes, frag_hashes, fids);
+    return process_host(r, c->devs[g], objs, lens, nobj, segment, frags_out, seg_hashes, frag_hashes, fids);
 }
 
 }  // extern "C"

@@ -81,17 +81,41 @@ std::vector<uint64_t> rs_table(const uint8_t* rows, int nout, int k) {
 
 }  // namespace
 
+namespace {
+
+// One call lane's rs scratch: rs calls on different lanes of the first GPU run concurrently
+// (dm_ctx call lanes), each with its own staging, so two uploads' FullProcessing overlap.
+struct RsLane {
+    DevBuf dec_tab;             // per reconstruct call
+    DevBuf work;                // host-API shard staging, process parity, FullProcessing windows
+    PinnedBuf fp_slot[4];       // dm_full_processing: file / parity slots (fullproc_capi.inl)
+};
+
+}  // namespace
+
 struct dm_rs {
     dm_ctx* c = nullptr;
     int k = 0, m = 0;
     std::vector<uint8_t> mat;   // (k + m) x k
-    DevBuf enc_tab;             // parity rows, k x 256 x 8 B
-    DevBuf dec_tab;             // per reconstruct call
-    DevBuf work;                // host-API shard staging
-    PinnedBuf fp_slot[4];       // dm_full_processing: file / parity slots (fullproc_capi.inl)
+    DevBuf enc_tab;             // parity rows, k x 256 x 8 B (read-only after dm_rs_create)
+    std::vector<RsLane> ln;     // one per call lane of the context's first GPU
 };
 
 namespace {
+
+// Lane of the context's first GPU (where an rs lives) for an rs call, counted in its load like
+// pick_device (the caller's CallLock(..., kReserved) releases it).
+int rs_lane(dm_ctx* c) {
+    std::lock_guard<std::mutex> lk(c->route_mu);
+    const int g = pick_lane_of(c, 0);
+    c->slots[g].load++;
+    return g;
+}
+
+// The rs scratch of the lane d belongs to (d is one of r->c->devs, on the first GPU).
+RsLane& rs_ln(dm_rs* r, const Dev& d) {
+    return r->ln[(size_t)(&d - r->c->devs.data()) / (size_t)r->c->nphys];
+}
 
 void launch_rs(Dev& d, hipStream_t s, int k, const dm::RsArgs& a) {
     const uint64_t units = a.units_per_seg;
@@ -153,14 +177,15 @@ int rs_reconstruct_dev(dm_rs* r, Dev& d, hipStream_t s, uint8_t* const* shards, 
     if (nmiss == 0) return DM_OK;
     const std::vector<uint64_t> tab = rs_table(rows.data(), nmiss, r->k);
     RC_TRY(tables_begin(c, d, tab.size() * 8));
-    RC_TRY(upload(c, d, s, r->dec_tab, tab.data(), tab.size() * 8));
+    RsLane& L = rs_ln(r, d);
+    RC_TRY(upload(c, d, s, L.dec_tab, tab.data(), tab.size() * 8));
     dm::RsArgs a{};
     for (int j = 0; j < r->k; j++) a.in[j] = shards[valid[j]];
     for (int t = 0; t < nmiss; t++) a.out[t] = shards[missing[t]];
     a.in_seg_stride = a.out_seg_stride = pitch;
     a.units_per_seg = nbytes_units;
     a.nseg = 1;
-    a.table = static_cast<const uint2*>(r->dec_tab.p);
+    a.table = static_cast<const uint2*>(L.dec_tab.p);
     a.nout = (uint32_t)nmiss;
     launch_rs(d, s, r->k, a);
     HIP_TRY(hipGetLastError());
@@ -204,10 +229,14 @@ int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
         }
     const std::vector<uint64_t> tab = rs_table(r->mat.data() + (size_t)k * k, parity_shards, k);
     Dev& d = ctx->devs[0];
-    for (DevBuf* b : {&r->enc_tab, &r->dec_tab, &r->work}) {
-        b->rp = &ctx->reaper;   // growth (r->work: FullProcessing windows) never synchronises the device
-        b->dev = d.id;
-    }
+    r->ln.resize((size_t)ctx->lanes);
+    r->enc_tab.rp = &ctx->reaper;
+    r->enc_tab.dev = d.id;
+    for (RsLane& L : r->ln)
+        for (DevBuf* b : {&L.dec_tab, &L.work}) {
+            b->rp = &ctx->reaper;   // growth (work: FullProcessing windows) never synchronises the device
+            b->dev = d.id;
+        }
     hipError_t e = hipSetDevice(d.id);
     if (e == hipSuccess) e = r->enc_tab.ensure(tab.size() * 8);
     if (e == hipSuccess) e = hipMemcpy(r->enc_tab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
@@ -223,13 +252,15 @@ int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
 void dm_rs_destroy(dm_rs* r) {
     if (!r) return;
     {
-        CallLock lk(r->c, 0);
+        RangeLock lk(r->c);   // after every call in flight on any lane
         (void)hipSetDevice(r->c->devs[0].id);
         (void)hipDeviceSynchronize();
         r->enc_tab.release();
-        r->dec_tab.release();
-        r->work.release();
-        for (auto& b : r->fp_slot) b.release();
+        for (RsLane& L : r->ln) {
+            L.dec_tab.release();
+            L.work.release();
+            for (auto& b : L.fp_slot) b.release();
+        }
     }
     delete r;
 }
@@ -244,11 +275,12 @@ int dm_rs_encode_device_async(dm_rs* r, const void* data, uint64_t data_stride, 
                               uint64_t shard, uint64_t nseg, void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (!data || !parity || nseg == 0 || shard == 0 || shard % 16 || data_stride % 16 || parity_stride % 16 ||
         !is_aligned16(data) || !is_aligned16(parity))
         return fail(c, DM_ERR_INVALID, "dm_rs_encode_device_async: need 16-byte aligned shards, strides and sizes");
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     dm::RsArgs a{};
@@ -275,13 +307,14 @@ int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t*
                                    void* stream) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (!shards || !present || shard == 0 || shard % 16)
         return fail(c, DM_ERR_INVALID, "dm_rs_reconstruct_device_async: shard bytes must be a multiple of 16");
     for (int i = 0; i < r->k + r->m; i++)
         if (!shards[i] || !is_aligned16(shards[i]))
             return fail(c, DM_ERR_INVALID, "dm_rs_reconstruct_device_async: shard %d null or not 16-byte aligned", i);
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
     hipStream_t s = pick_stream(d, stream);
     RC_TRY(begin_call(c, d, s));
     return rs_reconstruct_dev(r, d, s, reinterpret_cast<uint8_t* const*>(shards), present, shard, shard / 16);
@@ -292,23 +325,25 @@ int dm_rs_reconstruct_device_async(dm_rs* r, void* const* shards, const uint8_t*
 int dm_rs_encode(dm_rs* r, const void* const* data, void* const* parity, uint64_t shard) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     if (!data || !parity || shard == 0) return fail(c, DM_ERR_INVALID, "dm_rs_encode: null shards or zero size");
     for (int j = 0; j < r->k; j++)
         if (!data[j]) return fail(c, DM_ERR_INVALID, "dm_rs_encode: data shard %d is null", j);
     for (int i = 0; i < r->m; i++)
         if (!parity[i]) return fail(c, DM_ERR_INVALID, "dm_rs_encode: parity shard %d is null", i);
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
+    DevBuf& work = rs_ln(r, d).work;
     hipStream_t s = d.stream;
     RC_TRY(begin_call(c, d, s));
     const uint64_t pitch = round_up(shard, 16);
     const int total = r->k + r->m;
-    HIP_TRY(r->work.ensure(pitch * total));
+    HIP_TRY(work.ensure(pitch * total));
     for (int j = 0; j < r->k; j++)
-        HIP_TRY(hipMemcpyAsync(r->work.u8() + j * pitch, data[j], shard, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(work.u8() + j * pitch, data[j], shard, hipMemcpyHostToDevice, s));
     dm::RsArgs a{};
-    for (int j = 0; j < r->k; j++) a.in[j] = r->work.u8() + j * pitch;
-    for (int i = 0; i < r->m; i++) a.out[i] = r->work.u8() + (r->k + i) * pitch;
+    for (int j = 0; j < r->k; j++) a.in[j] = work.u8() + j * pitch;
+    for (int i = 0; i < r->m; i++) a.out[i] = work.u8() + (r->k + i) * pitch;
     a.in_seg_stride = a.out_seg_stride = 0;
     a.units_per_seg = pitch / 16;
     a.nseg = 1;
@@ -317,7 +352,7 @@ int dm_rs_encode(dm_rs* r, const void* const* data, void* const* parity, uint64_
     launch_rs(d, s, r->k, a);
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < r->m; i++)
-        HIP_TRY(hipMemcpyAsync(parity[i], r->work.u8() + (r->k + i) * pitch, shard, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(parity[i], work.u8() + (r->k + i) * pitch, shard, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     return DM_OK;
 }
@@ -342,7 +377,8 @@ int dm_rs_encode_buffer(dm_rs* r, const void* host, uint64_t len, void* out, uin
 int dm_rs_reconstruct(dm_rs* r, void* const* shards, const uint8_t* present, uint64_t shard) {
     if (!r) return bad_arg();
     dm_ctx* c = r->c;
-    CallLock lk(c, 0);
+    const int g = rs_lane(c);
+    CallLock lk(c, g, kReserved);
     const int total = r->k + r->m;
     if (!shards || !present || shard == 0) return fail(c, DM_ERR_INVALID, "dm_rs_reconstruct: bad arguments");
     for (int i = 0; i < total; i++)
@@ -351,14 +387,15 @@ int dm_rs_reconstruct(dm_rs* r, void* const* shards, const uint8_t* present, uin
     for (int i = 0; i < total; i++) nv += present[i] != 0;
     if (nv == total) return DM_OK;
     if (nv < r->k) return fail(c, DM_ERR_INVALID, "too few shards given (%d of %d needed)", nv, r->k);
-    Dev& d = c->devs[0];
+    Dev& d = c->devs[g];
+    DevBuf& work = rs_ln(r, d).work;
     hipStream_t s = d.stream;
     RC_TRY(begin_call(c, d, s));
     const uint64_t pitch = round_up(shard, 16);
-    HIP_TRY(r->work.ensure(pitch * total));
+    HIP_TRY(work.ensure(pitch * total));
     std::vector<uint8_t*> dev(total);
     for (int i = 0; i < total; i++) {
-        dev[i] = r->work.u8() + i * pitch;
+        dev[i] = work.u8() + i * pitch;
         if (present[i]) HIP_TRY(hipMemcpyAsync(dev[i], shards[i], shard, hipMemcpyHostToDevice, s));
     }
     RC_TRY(rs_reconstruct_dev(r, d, s, dev.data(), present, pitch, pitch / 16));

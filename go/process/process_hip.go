@@ -10,7 +10,7 @@
 //     process-wide dm_batcher, which coalesces whatever concurrent handler goroutines have queued
 //     into one batched GPU pass (dm_batcher_process); Go memory is bounded process-wide (1 GiB
 //     per call in flight, DEOSS_PROCESS_MEM_GIB (default 8) at once, buffers pooled);
-//   - larger files: dm_full_processing on a per-GPU pipeline, which reads the file, writes every
+//   - larger files: dm_full_processing on a lane of a per-GPU pipeline, which reads the file, writes every
 //     fragment and segment file itself and overlaps those writes with the GPU's coding and hashing
 //     (one GPU pass per 32 GiB of file, no Go memory for the data);
 //   - cipher != "" (an encrypted upload, the Cipher header of node/objectHandler.go:102 and
@@ -56,7 +56,7 @@ var (
 	initEr  error
 	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
 	bufs    sync.Pool     // *windowBuf, reused across calls
-	pipes   chan *C.dm_rs // large files: one dm_full_processing pipeline per GPU
+	pipes   chan *C.dm_rs // large files: each GPU's pipeline, once per call lane of its context
 	coders  []*C.dm_rs    // the same pipelines, for streams (NewWriter picks one round robin)
 	nextW   atomic.Uint64
 	// writeSegments: SegmentHash paths exist as files (the zero-padded segment bytes), like the
@@ -86,7 +86,7 @@ func gpu() error {
 			initEr = errors.New(C.GoString(C.dm_strerror(C.DM_ERR_NODEV)))
 			return
 		}
-		pipes = make(chan *C.dm_rs, ngpu)
+		pipes = make(chan *C.dm_rs, ngpu*8)
 		for g := 0; g < ngpu; g++ {
 			var pc *C.dm_ctx
 			var rs *C.dm_rs
@@ -99,7 +99,11 @@ func gpu() error {
 				initEr = errors.New(C.GoString(C.dm_strerror(rc)))
 				return
 			}
-			pipes <- rs
+			// one token per call lane: a coder's calls run on its context's lanes (own staging each),
+			// so that many large uploads share the GPU side by side (DEOSS_LANES, default 2)
+			for l := 0; l < int(C.dm_lane_count(pc)); l++ {
+				pipes <- rs
+			}
 			coders = append(coders, rs)
 		}
 		// every visible GPU, 2 worker slots each, 4096 leaves per batch, 2 ms linger (DESIGN.md §6.9)
@@ -247,7 +251,7 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 	return info, hex.EncodeToString(w.fid[:]), nil
 }
 
-// fullProcessingLarge: one dm_full_processing call on a free per-GPU pipeline.  The library reads
+// fullProcessingLarge: one dm_full_processing call on a free pipeline lane.  The library reads
 // the file, writes every fragment and segment file to savedir/<hex SHA-256> (data fragments while
 // the file is still being read, parity fragments while the leaf kernel hashes) and returns the
 // digests and the fid.

@@ -699,10 +699,14 @@ int main(int argc, char** argv) {
     for (auto& x : th) x.join();
 
     dm_destroy(c);
-    if (fails) {
-        std::fprintf(stderr, "%d failures\n", fails.load());
-        return 1;
-    }
-    std::printf("PASS\n");
-    return 0;
+    const int status = fails ? 1 : 0;
+    if (fails) std::fprintf(stderr, "%d failures\n", fails.load());
+    else std::printf("PASS\n");
+    std::fflush(stdout);
+    // ASan leg (run_host_tests.sh): every context is destroyed by now.  Exit without the runtime's
+    // exit-time teardown: under ASan, device chunks freed during the run wait in ASan's quarantine,
+    // and one recycled after the HSA runtime has unloaded trips ASan's own device-allocator CHECK
+    // (sanitizer_allocator_device.h, "dev_runtime_unloaded_"), inside HSA's teardown, not ours.
+    if (std::getenv("DEOSS_TEST_QUICK_EXIT")) std::_Exit(status);
+    return status;
 }

@@ -181,6 +181,76 @@ def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, monke
     p.close()
 
 
+def test_process_lanes_concurrent(oracle_lib, tmp_path):
+    """rs calls on call lanes: one coder on a 3-lane context, 9 threads mixing FullProcessing from
+    files (own savedirs), dm_process_buffer, Encode and Reconstruct, each with its lane's own rs
+    staging; then two 5-segment files at chain.SegmentSize through dm_full_processing at once
+    (striped windows, pooled kits per lane).  Everything vs the oracle."""
+    import threading
+    from deoss_amd import MerkleContext
+    from deoss_amd.process import Processor
+    from deoss_amd.reedsolomon import Encoder
+    from oracle import splitmix64_bytes
+    ctx = MerkleContext(lanes=3)
+    p = Processor(ctx, 4, 8, 4096)
+    enc = Encoder(ctx, 4, 8)
+    errors = []
+
+    def worker(t):
+        try:
+            for i in range(3):
+                data = splitmix64_bytes(7 * 4096 + 131 * (3 * t + i) + 1, 0xDE0553000 + 3 * t + i)
+                want_seg, want_frag, want_fid, want_frags = oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
+                kind = (t + i) % 3
+                if kind == 0:
+                    f = tmp_path / f"obj_{t}_{i}.bin"
+                    f.write_bytes(data)
+                    got = p.full_processing_file(str(f), str(tmp_path / f"cache_{t}_{i}"))
+                    ok = got == (want_seg, want_frag, want_fid)
+                elif kind == 1:
+                    seg, frag, fid, frags = p.process_buffer(data)
+                    ok = (seg, frag, fid, frags) == (want_seg, want_frag, want_fid, want_frags)
+                else:
+                    shards = enc.Split(data[:4096 * 2])
+                    full = enc.Encode(shards)
+                    rebuilt = enc.Reconstruct([None if j in (0, 5, 9, 11) else s for j, s in enumerate(full)])
+                    ok = rebuilt == full and enc.Verify(full)
+                if not ok:
+                    errors.append((t, i, kind))
+        except Exception as e:   # reported below
+            errors.append((t, repr(e)))
+
+    try:
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(9)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert errors == []
+        big = Processor(ctx)
+        datas = [splitmix64_bytes(5 * (32 << 20) - 77 * (j + 1), 0xDE0553100 + j) for j in range(2)]
+        outs = [None, None]
+
+        def fp(j):
+            f = tmp_path / f"big_{j}.bin"
+            f.write_bytes(datas[j])
+            outs[j] = big.full_processing_file(str(f), str(tmp_path / f"bigcache_{j}"))
+
+        th = [threading.Thread(target=fp, args=(j,)) for j in range(2)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        for j in range(2):
+            want = oracle_lib.full_processing(datas[j], 32 << 20, 4, 8, nthreads=8)[:3]
+            assert outs[j] == want, j
+        big.close()
+    finally:
+        enc.close()
+        p.close()
+        ctx.close()
+
+
 def _pieces(data, rng, most):
     pos = 0
     while pos < len(data):

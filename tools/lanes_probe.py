@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--threads", default="1,2,4")
     ap.add_argument("--lanes", default="1,2,4")
     ap.add_argument("--workloads", default="pinned8g,pageable2g,pinned1m")
+    ap.add_argument("--fp-gib", type=float, default=1.0, help="FullProcessing file size (0: skip)")
     args = ap.parse_args()
     import torch
     from deoss_amd import MerkleContext
@@ -38,7 +39,7 @@ def main():
     }
     threads = [int(x) for x in args.threads.split(",")]
     lanes = [int(x) for x in args.lanes.split(",")]
-    for name in args.workloads.split(","):
+    for name in filter(None, args.workloads.split(",")):
         length, chunk, pinned = shapes[name]
         host = torch.empty(length, dtype=torch.uint8, pin_memory=pinned)
         dev = torch.empty(length, dtype=torch.uint8, device="cuda")
@@ -84,6 +85,63 @@ def main():
                                       "GiBps": round(T * length / gib / (wall / 1e3), 3),
                                       "roots_match": all(r == want for r in roots)}), flush=True)
         del host
+    if args.fp_gib:
+        full_processing(args, torch, threads, lanes)
+
+
+def full_processing(args, torch, threads, lanes):
+    """T threads each run dm_full_processing on their own file (own savedir) through one coder on
+    a context of V lanes: with V = 1 the calls queue on the coder's one lane."""
+    import shutil
+    import tempfile
+    from deoss_amd import MerkleContext
+    from deoss_amd.process import Processor
+    length = int(args.fp_gib * (1 << 30))
+    tmp = tempfile.mkdtemp(prefix="lanes_fp_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        T = max(threads)
+        with MerkleContext() as c0:
+            dev = torch.empty(length, dtype=torch.uint8, device="cuda")
+            for i in range(T):
+                c0.fill_synthetic_async(dev.data_ptr(), 0, length, 0xF00 + i, 0)
+                torch.cuda.synchronize()
+                with open(os.path.join(tmp, f"in_{i}"), "wb") as f:
+                    f.write(dev.cpu().numpy().tobytes())
+            del dev
+            torch.cuda.empty_cache()
+        want = None
+        for V in lanes:
+            ctx = MerkleContext(lanes=V)
+            p = Processor(ctx)
+            p.full_processing_file(os.path.join(tmp, "in_0"), os.path.join(tmp, "warm"))
+            ref = p.full_processing_file(os.path.join(tmp, "in_0"), os.path.join(tmp, "warm"))[2]
+            want = want or ref
+            for Tn in threads:
+                fids = [None] * Tn
+                go = threading.Barrier(Tn + 1)
+
+                def work(i):
+                    go.wait()
+                    fids[i] = p.full_processing_file(os.path.join(tmp, f"in_{i}"), os.path.join(tmp, f"out_{V}_{Tn}_{i}"))[2]
+
+                th = [threading.Thread(target=work, args=(i,)) for i in range(Tn)]
+                for t in th:
+                    t.start()
+                go.wait()
+                t0 = time.perf_counter()
+                for t in th:
+                    t.join()
+                wall = (time.perf_counter() - t0) * 1e3
+                for i in range(Tn):
+                    shutil.rmtree(os.path.join(tmp, f"out_{V}_{Tn}_{i}"), ignore_errors=True)
+                print(json.dumps({"workload": "full_processing_file", "bytes": length, "lanes": V, "threads": Tn,
+                                  "wall_ms": round(wall, 1),
+                                  "GiBps": round(Tn * length / (1 << 30) / (wall / 1e3), 3),
+                                  "fid0_matches": fids[0] == want}), flush=True)
+            p.close()
+            ctx.close()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 if __name__ == "__main__":
