@@ -487,7 +487,7 @@ def _summary(r):
         if k in r:
             keep[k] = r[k]
     for k in ("k1_avg_ms", "tail_ms_after_last_write", "leaf_kernel", "cpu", "gpu", "streamed", "after_file_saved",
-              "at_10GbE"):
+              "at_10GbE", "fragment_lookup"):
         if k in r:
             keep[k] = r[k]
     if "leaf_kernel" in r.get("config", {}):
@@ -1095,6 +1095,23 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
         parity = {"fid": fid.hex(), "segment_digests": nseg, "fragment_digests_checked_segments": sorted({0, nseg - 1}),
                   "files_on_disk": len(names), "files_expected": len(expect), "files_hash_checked": len(sample),
                   "bit_exact": bool(segd == want_seg and fid == orc.reduce(want_seg)[:32] and frag_ok and files_ok)}
+        # the download handler's question (node/fileHandler.go:962-979): one fragment by its name.
+        # dm_fragment_lookup vs the FullProcessing call the handler makes for it; bytes checked
+        # against the fragment file FullProcessing just wrote
+        lookup = {}
+        for tag, t_idx in [("last_fragment", nseg * total - 1), ("first_segment_parity", k)]:
+            name = fragd[32 * t_idx:32 * t_idx + 32].hex()
+            best, got = None, None
+            for _ in range(2):
+                t0 = time.perf_counter()
+                got = proc.fragment_lookup(path, name)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            with open(os.path.join(savedir, name), "rb") as fh:
+                ok = got is not None and got[:2] == (t_idx // total, t_idx % total) and got[2] == fh.read()
+            lookup[tag] = {"ms": round(best * 1e3, 1), "speedup_vs_full_processing": round(tavg / best, 2),
+                           "bit_exact": bool(ok)}
+        parity["fragment_lookup_bit_exact"] = all(v["bit_exact"] for v in lookup.values())
         # the window path, same file, same savedir state
         fresh()
         t0 = time.perf_counter()
@@ -1147,6 +1164,9 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
                        "object_bytes": length, "output_bytes": out_bytes},
             "step_ms": [round(t * 1e3, 1) for t in times],
             "leaf_kernel_avg_ms": round(k_avg, 3),
+            "fragment_lookup": dict(lookup, what="dm_fragment_lookup: the one fragment the download handler serves, "
+                                    "found by name (file read in 1 GiB windows, RS + fragment hashes on the GPU, no files "
+                                    "written) instead of FullProcessing + scan"),
             "window_path": {"GiBps": round(length / t_win / (1 << 30), 4), "ms": round(t_win * 1e3, 1),
                             "what": "read 8 segments, dm_process_buffer, write their files from Python, repeat"},
             "host_io_floor": None if floor is None else {

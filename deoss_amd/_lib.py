@@ -37,7 +37,7 @@ EXPORTS = (
     "dm_timing_summary",
     "dm_rs_create", "dm_rs_destroy", "dm_rs_matrix", "dm_rs_encode", "dm_rs_encode_buffer", "dm_rs_reconstruct",
     "dm_rs_verify", "dm_rs_encode_device_async", "dm_rs_reconstruct_device_async",
-    "dm_process_device_async", "dm_process_buffer", "dm_process_batch", "dm_full_processing",
+    "dm_process_device_async", "dm_process_buffer", "dm_process_batch", "dm_full_processing", "dm_fragment_lookup",
     "dm_pstream_open", "dm_pstream_write", "dm_pstream_close", "dm_pstream_abort",
     "dm_tree_node_count", "dm_tree_depth", "dm_tree_levels_device_async", "dm_tree_levels",
     "dm_merkle_paths_device_async", "dm_merkle_paths", "dm_verify_paths_device_async", "dm_verify_paths",
@@ -106,6 +106,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_process_buffer": ([vp, vp, u64, u64, vp, vp, vp, vp], i32),
         "dm_process_batch": ([vp, pvp, pu64, u64, u64, pvp, pvp, pvp, vp], i32),
         "dm_full_processing": ([vp, ctypes.c_char_p, ctypes.c_char_p, u64, i32, vp, vp, u64, pu64, vp], i32),
+        "dm_fragment_lookup": ([vp, ctypes.c_char_p, u64, vp, vp, u64, ctypes.POINTER(i32), pu64,
+                                ctypes.POINTER(i32)], i32),
         "dm_pstream_open": ([vp, u64, ctypes.c_char_p, i32, ctypes.POINTER(vp)], i32),
         "dm_pstream_write": ([vp, vp, u64], i32),
         "dm_pstream_close": ([vp, vp, vp, u64, pu64, vp], i32),

@@ -1687,6 +1687,7 @@ int dm_root_batch(dm_ctx* ctx, const void* const* objs, const uint64_t* lens, ui
 #include "rs_capi.inl"
 #include "process_capi.inl"
 #include "fullproc_capi.inl"
+#include "fragment_capi.inl"
 #include "process_stream.inl"
 #include "tree_capi.inl"
 #include "batcher.inl"

@@ -163,6 +163,27 @@ class Processor:
             return seg.raw[:32 * n], frag.raw[:32 * n * total], fid.raw
         raise DeossMerkleError(DM_ERR_INVALID, "dm_full_processing: file size changed during the call")
 
+    def fragment_lookup(self, file: str, fragment_hash: str, want_bytes: bool = True
+                        ) -> Optional[Tuple[int, int, Optional[bytes]]]:
+        """``dm_fragment_lookup``: the fragment of ``file`` named ``fragment_hash`` (hex SHA-256), as
+        the download handler finds it (node/fileHandler.go:962-979) -- without writing any file.
+        Returns (segment index, fragment index, fragment bytes or None), or None when no fragment of
+        the file has that name."""
+        L = self.ctx._L
+        want = bytes.fromhex(fragment_hash)
+        if len(want) != 32:
+            raise ValueError("fragment hash must be 32 bytes of hex")
+        out = ctypes.create_string_buffer(self.frag) if want_bytes else None
+        found, seg_i, frag_i = ctypes.c_int(0), ctypes.c_uint64(0), ctypes.c_int(0)
+        rc = L.dm_fragment_lookup(self.enc._h, os.fsencode(file), self.segment, want, out, self.frag if out else 0,
+                                  ctypes.byref(found), ctypes.byref(seg_i), ctypes.byref(frag_i))
+        if rc == DM_ERR_IO:
+            raise DeossMerkleError(rc, (L.dm_last_error(None) or b"").decode())
+        self._check(rc, "dm_fragment_lookup")
+        if not found.value:
+            return None
+        return seg_i.value, frag_i.value, (out.raw if out is not None else None)
+
     def FullProcessing(self, file: str, cipher: str, savedir: str
                        ) -> Tuple[Optional[List[SegmentDataInfo]], str, Optional[Exception]]:
         """FullProcessing in one library call (``dm_full_processing``: reads, coding, hashing and
@@ -341,3 +362,16 @@ def FullProcessing(file: str, cipher: str, savedir: str
         except DeossMerkleError as e:   # no GPU: the Go shape (nil, "", err), as gpu() fails in Go
             return None, "", e
     return _default.FullProcessing(file, cipher, savedir)
+
+
+def FindFragment(fpath: str, fragment_hash: str) -> Tuple[Optional[bytes], Optional[Exception]]:
+    """process.FindFragment (go/process/process_hip.go) on the default GPU pipeline: the fragment
+    of ``fpath`` named ``fragment_hash``, or (None, None) when the file has no such fragment."""
+    global _default
+    try:
+        if _default is None:
+            _default = Processor()
+        hit = _default.fragment_lookup(fpath, fragment_hash)
+    except (DeossMerkleError, ValueError) as e:
+        return None, e
+    return (hit[2] if hit else None), None

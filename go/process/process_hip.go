@@ -306,3 +306,43 @@ func fullProcessingLarge(file, savedir string, nseg uint64) ([]chain.SegmentData
 		return info, hex.EncodeToString(fid[:]), nil
 	}
 }
+
+// FindFragment (additive, for the fragment download handler, node/fileHandler.go:962-979): the
+// fragment of the file at fpath whose name is fragmentHash (hex SHA-256), found without writing
+// every fragment to a cache directory first (dm_fragment_lookup: the file is RS-coded and its
+// fragments hashed on the GPU window by window, and the scan stops at the window holding the name).
+// Returns (nil, nil) when no fragment of the file has that name, as the handler's scan falls
+// through to the chain.  The first match in (segment, index) order wins, as in the handler.
+func FindFragment(fpath, fragmentHash string) ([]byte, error) {
+	want, err := hex.DecodeString(fragmentHash)
+	if err != nil || len(want) != 32 {
+		return nil, errors.New("invalid fragment hash")
+	}
+	if err := gpu(); err != nil {
+		return nil, err
+	}
+	rs := <-pipes
+	defer func() { pipes <- rs }()
+	out := make([]byte, uint64(chain.SegmentSize)/uint64(chain.DataShards))
+	cpath := C.CString(fpath)
+	defer C.free(unsafe.Pointer(cpath))
+	var found, idx C.int
+	var seg C.uint64_t
+	runtime.LockOSThread() // dm_last_error is thread-local: call and read on one OS thread
+	defer runtime.UnlockOSThread()
+	rc := C.dm_fragment_lookup(rs, cpath, C.uint64_t(chain.SegmentSize), (*C.uint8_t)(unsafe.Pointer(&want[0])),
+		unsafe.Pointer(&out[0]), C.uint64_t(len(out)), &found, &seg, &idx)
+	if rc != C.DM_OK {
+		if rc == C.DM_ERR_EMPTY {
+			return nil, errors.New("Empty data")
+		}
+		if msg := C.GoString(C.dm_last_error(nil)); msg != "" {
+			return nil, errors.New(msg)
+		}
+		return nil, errors.New(C.GoString(C.dm_strerror(rc)))
+	}
+	if found == 0 {
+		return nil, nil
+	}
+	return out, nil
+}

@@ -240,6 +240,17 @@ int dm_process_batch(dm_rs *rs, const void *const *objs, const uint64_t *lens, u
 #define DM_FP_SEGMENT_FILES 1
 int dm_full_processing(dm_rs *rs, const char *path, const char *savedir, uint64_t segment, int flags,
                        uint8_t *seg_hashes, uint8_t *frag_hashes, uint64_t cap, uint64_t *nseg_out, uint8_t fid[32]);
+/* The fragment download path (node/fileHandler.go:958-1013) runs FullProcessing(fpath, "", cacheDir)
+ * over a locally held object only to serve the ONE fragment whose name (hex SHA-256) was asked for.
+ * This finds it without writing anything: the file is read window by window (double-buffered with
+ * the GPU), segments are RS-coded and every fragment hashed on the device (no segment hashes, no
+ * fid, no files), and the scan stops at the first window holding `want`.  *found = 1 with the
+ * fragment's (segment, index) (data fragments 0 .. data-1, then parity) and, when out != NULL, its
+ * segment/data bytes in out (out_cap >= that); *found = 0 when no fragment has that name.  The
+ * first match in (segment, index) order wins, as the handler's scan.  Errors as dm_full_processing
+ * ("open <path>: ...", "Empty data"). */
+int dm_fragment_lookup(dm_rs *rs, const char *path, uint64_t segment, const uint8_t want[32], void *out,
+                       uint64_t out_cap, int *found, uint64_t *seg_idx, int *frag_idx);
 
 /* FullProcessing while the upload body arrives (SURVEY.md 8f #1 + #2): the handlers write the body
  * to a file (node/objectHandler.go:248-266, node/fileHandler.go:899-937) and then run

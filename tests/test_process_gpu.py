@@ -181,6 +181,58 @@ def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, monke
     p.close()
 
 
+@pytest.mark.parametrize("window", [None, 3 * 4096, 4096])
+def test_fragment_lookup(ctx, oracle_lib, tmp_path, monkeypatch, window):
+    """dm_fragment_lookup (the download handler's one fragment, node/fileHandler.go:962-979): every
+    probed name is found at the oracle's (segment, index) with the oracle's bytes -- first, middle
+    parity, the zero-padded last segment's last fragment --, across window boundaries (one window,
+    3-segment windows, 1-segment windows); a repeated segment resolves to its first copy; an unknown
+    name is None; file errors keep Go's text; nothing is written next to the file."""
+    from oracle import splitmix64_bytes
+    if window:
+        monkeypatch.setenv("DEOSS_FL_WINDOW_BYTES", str(window))
+    p = _processor(ctx, 4, 8, 4096)
+    data = splitmix64_bytes(10 * 4096 + 999, 0xDE0554000)
+    data = data[:4096] + data[:4096] + data[4096:]   # segments 0 and 1 identical
+    f = tmp_path / "object.bin"
+    f.write_bytes(data)
+    nseg = (len(data) + 4095) // 4096
+    _, frag_b, _, frags = oracle_lib.full_processing(data, 4096, 4, 8, want_frags=True)
+    for s, j in [(0, 0), (1, 3), (5, 9), (6, 4), (nseg - 1, 11), (nseg - 1, 0)]:
+        t = s * 12 + j
+        name = frag_b[32 * t:32 * t + 32].hex()
+        got = p.fragment_lookup(str(f), name)
+        want_s = 0 if s == 1 else s   # segment 1 repeats segment 0: the first copy wins
+        assert got == (want_s, j, frags[t * 1024:(t + 1) * 1024]), (s, j)
+        assert p.fragment_lookup(str(f), name, want_bytes=False) == (want_s, j, None)
+    assert p.fragment_lookup(str(f), "ab" * 32) is None
+    assert sorted(os.listdir(tmp_path)) == ["object.bin"]
+    with pytest.raises(Exception, match="no such file or directory"):
+        p.fragment_lookup(str(tmp_path / "missing"), "ab" * 32)
+    empty = tmp_path / "empty.bin"
+    empty.write_bytes(b"")
+    with pytest.raises(Exception, match="Empty data"):
+        p.fragment_lookup(str(empty), "ab" * 32)
+    p.close()
+
+
+def test_fragment_lookup_full_segments(ctx, oracle_lib, tmp_path, monkeypatch):
+    """chain.SegmentSize (32 MiB segments, 8 MiB fragments), 2-segment windows: the last segment's
+    last parity fragment and a data fragment of the second window, vs the oracle."""
+    from oracle import splitmix64_bytes
+    monkeypatch.setenv("DEOSS_FL_WINDOW_BYTES", str(64 << 20))
+    p = _processor(ctx)
+    data = splitmix64_bytes(5 * (32 << 20) + 12345, 0xDE0554100)
+    f = tmp_path / "object.bin"
+    f.write_bytes(data)
+    _, frag_b, _, frags = oracle_lib.full_processing(data, 32 << 20, 4, 8, want_frags=True, nthreads=8)
+    fr = 8 << 20
+    for s, j in [(5, 11), (2, 1)]:
+        t = s * 12 + j
+        assert p.fragment_lookup(str(f), frag_b[32 * t:32 * t + 32].hex()) == (s, j, frags[t * fr:(t + 1) * fr])
+    p.close()
+
+
 def test_process_lanes_concurrent(oracle_lib, tmp_path):
     """rs calls on call lanes: one coder on a 3-lane context, 9 threads mixing FullProcessing from
     files (own savedirs), dm_process_buffer, Encode and Reconstruct, each with its lane's own rs
