@@ -359,37 +359,23 @@ struct RangeLock {
 // CallLock(..., kReserved) or stream releases it): the GPU whose lanes carry the least load, ties
 // broken round-robin, then that GPU's least-loaded lane (lower lanes first).  Choice and count
 // happen under route_mu, so concurrent callers see each other's picks.
+// The lane loads of a context, lane-major (dm_plan::pick_lane's layout); caller holds route_mu.
+std::vector<int> lane_loads(dm_ctx* c) {
+    std::vector<int> v(c->devs.size());
+    for (size_t i = 0; i < v.size(); i++) v[i] = c->slots[i].load.load();
+    return v;
+}
+
 int pick_lane_of(dm_ctx* c, int p) {
-    int best = p, best_load = c->slots[p].load.load();
-    for (int l = 1; l < c->lanes; l++) {
-        const int i = l * c->nphys + p;
-        const int x = c->slots[i].load.load();
-        if (x < best_load) {
-            best = i;
-            best_load = x;
-        }
-    }
-    return best;
+    const std::vector<int> v = lane_loads(c);
+    return dm_plan::pick_lane(v.data(), c->nphys, c->lanes, 0, p);
 }
 
 int pick_device(dm_ctx* c) {
     std::lock_guard<std::mutex> lk(c->route_mu);
-    const int P = c->nphys;
-    int bp = 0;
-    if (P > 1) {
-        const int start = (int)(c->rr.fetch_add(1) % (uint32_t)P);
-        int best_load = -1;
-        for (int i = 0; i < P; i++) {
-            const int p = (start + i) % P;
-            int x = 0;
-            for (int l = 0; l < c->lanes; l++) x += c->slots[l * P + p].load.load();
-            if (best_load < 0 || x < best_load) {
-                bp = p;
-                best_load = x;
-            }
-        }
-    }
-    const int g = pick_lane_of(c, bp);
+    const int start = c->nphys > 1 ? (int)(c->rr.fetch_add(1) % (uint32_t)c->nphys) : 0;
+    const std::vector<int> v = lane_loads(c);
+    const int g = dm_plan::pick_lane(v.data(), c->nphys, c->lanes, start);
     c->slots[g].load++;
     return g;
 }

@@ -170,4 +170,33 @@ inline int route(uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, int G, 
     return best;
 }
 
+// Call lanes (dm_ctx): loads[l * nphys + p] = calls running or queued on lane l of GPU p (plus
+// open streams).  A call that can run anywhere goes to the GPU whose lanes carry the least load
+// (GPUs scanned from `start`, the first minimum wins, so ties rotate with `start`), then to that
+// GPU's least-loaded lane (the lowest lane on ties, so an idle GPU's lane 0 takes single calls).
+// phys >= 0 fixes the GPU (device-memory calls, rs coders).  Returns the lane's index into loads.
+inline int pick_lane(const int* loads, int nphys, int lanes, int start, int phys = -1) {
+    int p = phys;
+    if (p < 0) {
+        p = 0;
+        int best = -1;
+        for (int i = 0; i < nphys; i++) {
+            const int q = (start + i) % nphys;
+            int x = 0;
+            for (int l = 0; l < lanes; l++) x += loads[l * nphys + q];
+            if (best < 0 || x < best) {
+                best = x;
+                p = q;
+            }
+        }
+    }
+    int g = p, best = loads[p];
+    for (int l = 1; l < lanes; l++)
+        if (loads[l * nphys + p] < best) {
+            best = loads[l * nphys + p];
+            g = l * nphys + p;
+        }
+    return g;
+}
+
 }  // namespace dm_plan

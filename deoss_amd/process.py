@@ -375,3 +375,28 @@ def FindFragment(fpath: str, fragment_hash: str) -> Tuple[Optional[bytes], Optio
     except (DeossMerkleError, ValueError) as e:
         return None, e
     return (hit[2] if hit else None), None
+
+
+def FullProcessingFiles(files: List[str], cipher: str, savedir: str
+                        ) -> Tuple[List[Optional[List[SegmentDataInfo]]], List[str], List[Optional[Exception]]]:
+    """process.FullProcessingFiles (go/process/process_hip.go; the batch upload PUT /files,
+    node/filesHandler.go:197-207): every file's FullProcessing at once, results in file order; an
+    empty path is skipped (None, "", None)."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(files)
+    infos: List[Optional[List[SegmentDataInfo]]] = [None] * n
+    fids, errs = [""] * n, [None] * n
+
+    def one(i):
+        infos[i], fids[i], errs[i] = FullProcessing(files[i], cipher, savedir)
+
+    global _default
+    todo = [i for i in range(n) if files[i]]
+    if todo and _default is None:   # the default pipeline, made once before the calls start
+        try:
+            _default = Processor()
+        except DeossMerkleError as e:   # no GPU: every call fails the Go way
+            return [None] * n, [""] * n, [e if files[i] else None for i in range(n)]
+    with ThreadPoolExecutor(max(1, min(16, len(todo)))) as ex:
+        list(ex.map(one, todo))
+    return infos, fids, errs

@@ -251,6 +251,31 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 	return info, hex.EncodeToString(w.fid[:]), nil
 }
 
+// FullProcessingFiles (additive, for the batch upload PUT /files, node/filesHandler.go:197-207,
+// which calls FullProcessing once per file from one goroutine): every file's FullProcessing at
+// once, so small files share batched GPU passes (the process-wide batcher coalesces concurrent
+// calls) instead of paying one segment chain (~0.5 s) each in turn, and large files run on the
+// pipeline lanes side by side.  Results in file order, each exactly FullProcessing(files[i],
+// cipher, savedir); an empty path is skipped (nil, "", nil), as the handler skips failed files.
+func FullProcessingFiles(files []string, cipher string, savedir string) ([][]chain.SegmentDataInfo, []string, []error) {
+	infos := make([][]chain.SegmentDataInfo, len(files))
+	fids := make([]string, len(files))
+	errs := make([]error, len(files))
+	var wg sync.WaitGroup
+	for i := range files {
+		if files[i] == "" {
+			continue
+		}
+		wg.Add(1)
+		go func(i int) {
+			defer wg.Done()
+			infos[i], fids[i], errs[i] = FullProcessing(files[i], cipher, savedir)
+		}(i)
+	}
+	wg.Wait()
+	return infos, fids, errs
+}
+
 // fullProcessingLarge: one dm_full_processing call on a free pipeline lane.  The library reads
 // the file, writes every fragment and segment file to savedir/<hex SHA-256> (data fragments while
 // the file is still being read, parity fragments while the leaf kernel hashes) and returns the

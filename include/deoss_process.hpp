@@ -14,6 +14,7 @@
 #include <optional>
 #include <string>
 #include <tuple>
+#include <utility>
 #include <vector>
 
 #include "deoss_merkle.h"
@@ -128,6 +129,34 @@ inline Result FullProcessing(const std::string& file, const std::string& cipher,
         return {infos(savedir, segd, fragd, nseg), hex32(fid), std::nullopt};
     }
     return {{}, "", Error{DM_ERR_INVALID, "process: file size changed during the call"}};
+}
+
+// FindFragment(fpath, fragmentHash) (go/process: the download handler's one fragment,
+// node/fileHandler.go:962-979): the fragment bytes, an empty vector when the file has no fragment
+// of that name, or an error.  dm_fragment_lookup: nothing is written to disk.
+inline std::pair<std::vector<uint8_t>, std::optional<Error>> FindFragment(const std::string& fpath,
+                                                                          const std::string& fragment_hash) {
+    uint8_t want[32];
+    auto nib = [](char ch) -> int {
+        return ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
+    };
+    bool ok = fragment_hash.size() == 64;
+    for (int i = 0; ok && i < 32; i++) {
+        const int hi = nib(fragment_hash[2 * i]), lo = nib(fragment_hash[2 * i + 1]);
+        ok = hi >= 0 && lo >= 0;
+        want[i] = (uint8_t)(hi * 16 + lo);
+    }
+    if (!ok) return {{}, Error{DM_ERR_INVALID, "invalid fragment hash"}};
+    auto& p = Pipelines::instance();
+    dm_rs* rs = p.pick();
+    if (!rs) return {{}, Error{p.status(), dm_strerror(p.status())}};
+    std::vector<uint8_t> out(SegmentSize / DataShards);
+    int found = 0, idx = 0;
+    uint64_t seg = 0;
+    const int rc = dm_fragment_lookup(rs, fpath.c_str(), SegmentSize, want, out.data(), out.size(), &found, &seg, &idx);
+    if (rc != DM_OK) return {{}, last_error(rc)};
+    if (!found) out.clear();
+    return {std::move(out), std::nullopt};
 }
 
 // FullProcessing while the body arrives (dm_pstream_*): Write the pieces, then Close.

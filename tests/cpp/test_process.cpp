@@ -56,6 +56,21 @@ int main(int argc, char** argv) {
         EXPECT(got.size() == frag && std::memcmp(got.data(), obj.data() + frag, frag) == 0);
     }
 
+    // FindFragment (the download handler's one fragment): the same bytes FullProcessing wrote, by name
+    for (auto [s, j] : {std::pair<uint64_t, int>{0, 1}, {nseg - 1, 11}}) {
+        const std::string name = process::hex32(wf.data() + 32 * (s * 12 + j));
+        auto [bytes, ferr] = process::FindFragment(file, name);
+        std::ifstream in(dir + "/cache/" + name, std::ios::binary);
+        std::vector<uint8_t> disk((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+        EXPECT(!ferr && !bytes.empty() && bytes == disk);
+    }
+    {
+        auto [none, nerr] = process::FindFragment(file, std::string(64, 'a'));
+        EXPECT(!nerr && none.empty());
+        auto [bad, berr] = process::FindFragment(file, "xyz");
+        EXPECT(berr.has_value());
+    }
+
     // Writer: io.MultiWriter(f, w) in the handler; pieces of 1 B .. 5 MiB
     auto [w, werr] = process::Writer::New(dir + "/cache_stream");
     EXPECT(!werr && w);

@@ -130,6 +130,31 @@ int main(int argc, char** argv) {
     // the configured layouts (BASELINE configs[3]: 1 TiB at 32 MiB over 8 GPUs; weak scaling 256 per GPU)
     CHECK(dm_plan::plan_shards(32768, 8).k == 12 && dm_plan::plan_shards(32768, 8).nb == 8, "configs[3] layout");
     CHECK(dm_plan::plan_shards(2048, 8).k == 8 && dm_plan::plan_shards(2048, 8).nb == 8, "weak-scaling layout");
+    // 4. call lanes (dm_plan::pick_lane): loads are lane-major, loads[l * nphys + p]
+    {
+        const int idle[16] = {};
+        CHECK(dm_plan::pick_lane(idle, 8, 2, 0) == 0 && dm_plan::pick_lane(idle, 8, 2, 5) == 5, "idle: lane 0 of start");
+        CHECK(dm_plan::pick_lane(idle, 1, 4, 0) == 0, "one GPU idle: lane 0");
+        const int one[4] = {1, 0, 0, 0};                  // 1 GPU, 4 lanes, lane 0 busy
+        CHECK(dm_plan::pick_lane(one, 1, 4, 0) == 1, "lane 1 when lane 0 is busy");
+        const int two[4] = {1, 1, 0, 0};
+        CHECK(dm_plan::pick_lane(two, 1, 4, 0) == 2, "lowest idle lane");
+        const int full[2] = {3, 2};                       // 1 GPU, 2 lanes, both busy: the lighter one
+        CHECK(dm_plan::pick_lane(full, 1, 2, 0) == 1, "least-loaded lane");
+        // 2 GPUs x 2 lanes: GPU 0 carries 1 (lane 0), GPU 1 carries 2 -> GPU 0's idle lane 1
+        const int g2[4] = {1, 1, 0, 1};                   // lane 0: GPU0=1, GPU1=1; lane 1: GPU0=0, GPU1=1
+        CHECK(dm_plan::pick_lane(g2, 2, 2, 0) == 2 && dm_plan::pick_lane(g2, 2, 2, 1) == 2, "least-loaded GPU, then lane");
+        // 8 concurrent calls on 8 idle GPUs with rotating starts land on 8 different GPUs (lane 0)
+        int loads[16] = {};
+        for (int i = 0; i < 8; i++) loads[dm_plan::pick_lane(loads, 8, 2, i)]++;
+        bool spread = true;
+        for (int p = 0; p < 8; p++) spread &= loads[p] == 1 && loads[8 + p] == 0;
+        CHECK(spread, "8 calls over 8 GPUs");
+        for (int i = 0; i < 8; i++) loads[dm_plan::pick_lane(loads, 8, 2, i)]++;   // the next 8: every lane 1
+        for (int p = 0; p < 8; p++) spread &= loads[8 + p] == 1;
+        CHECK(spread, "16 calls over 16 lanes");
+        CHECK(dm_plan::pick_lane(loads, 8, 2, 3, 6) == 6, "fixed GPU: its lane 0 on ties");
+    }
     if (failures) {
         std::fprintf(stderr, "%d failure(s)\n", failures);
         return 1;

@@ -231,6 +231,43 @@ def test_fragment_lookup_full_segments(ctx, oracle_lib, tmp_path, monkeypatch):
         t = s * 12 + j
         assert p.fragment_lookup(str(f), frag_b[32 * t:32 * t + 32].hex()) == (s, j, frags[t * fr:(t + 1) * fr])
     p.close()
+    import deoss_amd.process as proc   # the Go-shaped mirror (go/process FindFragment)
+    t = 3 * 12 + 7
+    assert proc.FindFragment(str(f), frag_b[32 * t:32 * t + 32].hex()) == (frags[t * fr:(t + 1) * fr], None)
+    assert proc.FindFragment(str(f), "cd" * 32) == (None, None)
+    assert proc.FindFragment(str(f), "zz")[1] is not None
+
+
+def test_full_processing_files_batch_upload(oracle_lib, tmp_path):
+    """process.FullProcessingFiles (PUT /files, node/filesHandler.go:197-207): 12 files of 1 B ..
+    40 MiB (+ one skipped entry and one missing file), all at once: each result equals that
+    file's oracle FullProcessing, files on disk hash to their names, errors stay per file."""
+    import deoss_amd.process as proc
+    from oracle import splitmix64_bytes
+    sizes = [1, 4096, 100000, (1 << 20) + 3, 5 << 20, (32 << 20) - 1, 32 << 20, (40 << 20) + 7,
+             777, 65536, 3 << 20, 12345]
+    paths = []
+    for i, n in enumerate(sizes):
+        pth = tmp_path / f"f{i}.bin"
+        pth.write_bytes(splitmix64_bytes(n, 0xDE0555000 + i))
+        paths.append(str(pth))
+    paths.insert(3, "")
+    paths.append(str(tmp_path / "missing.bin"))
+    savedir = str(tmp_path / "cache")
+    infos, fids, errs = proc.FullProcessingFiles(paths, "", savedir)
+    assert len(infos) == len(fids) == len(errs) == len(paths)
+    assert (infos[3], fids[3], errs[3]) == (None, "", None)
+    assert errs[-1] is not None and fids[-1] == ""
+    for i, pth in enumerate(paths[:-1]):
+        if not pth:
+            continue
+        data = open(pth, "rb").read()
+        seg_b, frag_b, fid, _ = oracle_lib.full_processing(data, 32 << 20, 4, 8, nthreads=4)
+        assert errs[i] is None and fids[i] == fid.hex(), pth
+        nseg = len(seg_b) // 32
+        assert [os.path.basename(x.SegmentHash) for x in infos[i]] == [seg_b[32 * s:32 * s + 32].hex() for s in range(nseg)]
+        last = infos[i][-1].FragmentHash[-1]
+        assert hashlib.sha256(open(last, "rb").read()).hexdigest() == os.path.basename(last)
 
 
 def test_process_lanes_concurrent(oracle_lib, tmp_path):
