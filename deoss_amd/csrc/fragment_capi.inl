@@ -84,7 +84,10 @@ int dm_fragment_lookup(dm_rs* r, const char* path, uint64_t segment, const uint8
             if (frag_idx) *frag_idx = j;
             const uint8_t* src = j < k ? data[w % 2] + t * segment + (uint64_t)j * frag
                                        : par[w % 2] + t * pbytes + (uint64_t)(j - k) * frag;
-            return out && hipMemcpy(out, src, frag, hipMemcpyDeviceToHost) != hipSuccess ? -1 : 1;
+            if (!out) return 1;
+            const bool ok = hipMemcpyAsync(out, src, frag, hipMemcpyDeviceToHost, s) == hipSuccess &&
+                            hipStreamSynchronize(s) == hipSuccess;
+            return ok ? 1 : -1;
         }
         return 0;
     };

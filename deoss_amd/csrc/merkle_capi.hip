@@ -201,6 +201,10 @@ struct Dev {
     hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_htab = nullptr;
     hipStream_t last_stream = nullptr;  // stream of the last enqueued call (scratch ordering)
     bool has_last = false;
+    // end of the lane's last call on the GPU (recorded when its lock is released): an async call's
+    // kernels outlive its lock, so routing counts a lane whose tail has not completed as busy
+    hipEvent_t ev_tail = nullptr;
+    hipStream_t tail_stream = nullptr;  // set by begin_call, recorded into ev_tail at unlock
     // timing records: (K1 begin, K1 end, call end) per timed call, reused across resets
     std::vector<hipEvent_t> tev;
     size_t ntimed = 0;
@@ -315,19 +319,30 @@ struct DeviceRestore {
     DeviceRestore& operator=(const DeviceRestore&) = delete;
 };
 
-// An entry point's hold on ONE device of its context for the whole call (that device's scratch,
-// streams and staging), and the caller's device restored after.  Calls on different devices of one
+// The lane's tail: its last call's work ends with this event (begin_call set tail_stream; the
+// caller holds the lane's lock).
+void record_tail(Dev& d) {
+    if (!d.tail_stream) return;
+    if (hipSetDevice(d.id) == hipSuccess) (void)hipEventRecord(d.ev_tail, d.tail_stream);
+    (void)hipGetLastError();
+    d.tail_stream = nullptr;
+}
+
+// An entry point's hold on ONE lane of its context for the whole call (that lane's scratch,
+// streams and staging), and the caller's device restored after.  Calls on different lanes of one
 // context run concurrently; a thread holds at most one CallLock.
 constexpr bool kReserved = true;   // CallLock on a lane that pick_device / device_of already counted
 struct CallLock {
     DeviceRestore dev;
+    Dev* d;
     DevSlot* slot;
     std::unique_lock<std::mutex> lk;
-    CallLock(dm_ctx* c, int g, bool reserved = false) : slot(&c->slots[g]) {
+    CallLock(dm_ctx* c, int g, bool reserved = false) : d(&c->devs[g]), slot(&c->slots[g]) {
         if (!reserved) slot->load++;
         lk = std::unique_lock<std::mutex>(slot->mu);
     }
     ~CallLock() {
+        record_tail(*d);
         lk.unlock();
         slot->load--;
     }
@@ -335,8 +350,8 @@ struct CallLock {
     CallLock& operator=(const CallLock&) = delete;
 };
 
-// Devices [0, G) of a context, locked in index order (so two of these cannot deadlock): sharded
-// calls (G = the devices they use) and context-wide settings (G = every device).
+// Lanes [0, G) of a context, locked in index order (so two of these cannot deadlock): sharded
+// calls (G = the GPUs they use: lane 0 of each) and context-wide settings (G = every lane).
 struct RangeLock {
     DeviceRestore dev;
     dm_ctx* c;
@@ -348,6 +363,7 @@ struct RangeLock {
     }
     explicit RangeLock(dm_ctx* c_) : RangeLock(c_, (int)c_->devs.size()) {}
     ~RangeLock() {
+        for (int g = 0; g < G; g++) record_tail(c->devs[g]);
         for (auto& l : lks) l.unlock();
         for (int g = 0; g < G; g++) c->slots[g].load--;
     }
@@ -355,10 +371,6 @@ struct RangeLock {
     RangeLock& operator=(const RangeLock&) = delete;
 };
 
-// Lane for a call that can run anywhere, counted in its load before return (the caller's
-// CallLock(..., kReserved) or stream releases it): the GPU whose lanes carry the least load, ties
-// broken round-robin, then that GPU's least-loaded lane (lower lanes first).  Choice and count
-// happen under route_mu, so concurrent callers see each other's picks.
 // The lane loads of a context, lane-major (dm_plan::pick_lane's layout); caller holds route_mu.
 std::vector<int> lane_loads(dm_ctx* c) {
     std::vector<int> v(c->devs.size());
@@ -366,18 +378,32 @@ std::vector<int> lane_loads(dm_ctx* c) {
     return v;
 }
 
-int pick_lane_of(dm_ctx* c, int p) {
-    const std::vector<int> v = lane_loads(c);
-    return dm_plan::pick_lane(v.data(), c->nphys, c->lanes, 0, p);
+// Lane choice, counted in the lane's load before return (the caller's CallLock(..., kReserved) or
+// stream releases it): dm_plan::pick_lane over the calls running or queued per lane, GPU first
+// (least total load, ties round-robin from `start`), then within that GPU the lanes whose last
+// call's GPU work has not finished count one more (an async call's kernels outlive its lock, so
+// a second async caller goes to an idle lane instead of queueing behind them).  phys >= 0 fixes
+// the GPU.  Caller holds route_mu.
+int choose_lane(dm_ctx* c, int start, int phys) {
+    std::vector<int> v = lane_loads(c);
+    int g = dm_plan::pick_lane(v.data(), c->nphys, c->lanes, start, phys);
+    if (c->lanes > 1) {
+        const int p = g % c->nphys;
+        for (int l = 0; l < c->lanes; l++) {
+            const int i = l * c->nphys + p;
+            if (c->devs[i].ev_tail && hipEventQuery(c->devs[i].ev_tail) == hipErrorNotReady) v[i]++;
+        }
+        (void)hipGetLastError();
+        g = dm_plan::pick_lane(v.data(), c->nphys, c->lanes, start, p);
+    }
+    c->slots[g].load++;
+    return g;
 }
 
 int pick_device(dm_ctx* c) {
     std::lock_guard<std::mutex> lk(c->route_mu);
     const int start = c->nphys > 1 ? (int)(c->rr.fetch_add(1) % (uint32_t)c->nphys) : 0;
-    const std::vector<int> v = lane_loads(c);
-    const int g = dm_plan::pick_lane(v.data(), c->nphys, c->lanes, start);
-    c->slots[g].load++;
-    return g;
+    return choose_lane(c, start, -1);
 }
 
 // Calls already running or queued on the context (routing: a busy context never shards).
@@ -476,20 +502,19 @@ int device_of(dm_ctx* c, const void* p) {
         (void)hipGetLastError();
     }
     std::lock_guard<std::mutex> lk(c->route_mu);
-    const int g = pick_lane_of(c, phys);
-    c->slots[g].load++;
-    return g;
+    return choose_lane(c, 0, phys);
 }
 
 // Order this call's use of the context scratch after the previous call's (possibly other stream).
 int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
     HIP_TRY(hipSetDevice(d.id));
-    if (d.has_last && d.last_stream != s) {
-        HIP_TRY(hipEventRecord(d.ev_done, d.last_stream));
-        HIP_TRY(hipStreamWaitEvent(s, d.ev_done, 0));
-    }
+    // after the lane's previous call when that one ran on another stream: wait for its tail event
+    // (recorded when its lock was released), never for the old stream itself, which its caller
+    // may have destroyed since
+    if (d.has_last && d.last_stream != s) HIP_TRY(hipStreamWaitEvent(s, d.ev_tail, 0));
     d.last_stream = s;
     d.has_last = true;
+    d.tail_stream = s;
     return DM_OK;
 }
 
@@ -1013,8 +1038,24 @@ int init_device(dm_ctx* c, Dev& d) {
         b->dev = d.id;
     }
     HIP_TRY(hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id));
-    HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&d.copy, hipStreamNonBlocking));
+    // A process's ordinary HIP streams share GPU_MAX_HW_QUEUES (4) hardware queues per priority
+    // level, assigned least-used at creation, and a kernel or copy waits behind anything queued
+    // before it on its queue (tools/hwq_probe.hip; tools/conc_probe.hip: 4 normal streams run side
+    // by side, a 5th waits).  Which queue a lane would get then depends on every stream the process
+    // made before (torch's included): measured, two lanes' 0.5 s chains shared one queue after a
+    // caller had created 4 streams (profiles/r03/r03u_lanes.log).  A stream made with a CU mask gets
+    // a hardware queue of its own (conc_probe cumask: 8 such streams side by side after 8 ordinary
+    // ones), so each lane's compute stream is one, with every CU enabled.  Such streams synchronise
+    // with the legacy null stream (the library never uses it; a caller's stream-0 work orders with
+    // them).  The copy stream takes a lowest-priority queue: H2D copies never wait behind a chain.
+    int prio_least = 0, prio_greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+    {
+        std::vector<uint32_t> all_cus((size_t)(d.cus + 31) / 32, 0xffffffffu);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&d.stream, (uint32_t)all_cus.size(), all_cus.data()));
+    }
+    HIP_TRY(hipStreamCreateWithPriority(&d.copy, hipStreamNonBlocking, prio_least));
+    HIP_TRY(hipEventCreateWithFlags(&d.ev_tail, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_done, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_copy[0], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&d.ev_copy[1], hipEventDisableTiming));
@@ -1035,7 +1076,7 @@ void destroy_device(Dev& d) {
     d.stage[0].release();
     d.stage[1].release();
     d.htab.release();
-    for (hipEvent_t e : {d.ev_done, d.ev_copy[0], d.ev_copy[1], d.ev_step[0], d.ev_step[1], d.ev_htab})
+    for (hipEvent_t e : {d.ev_done, d.ev_copy[0], d.ev_copy[1], d.ev_step[0], d.ev_step[1], d.ev_htab, d.ev_tail})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : d.tev) (void)hipEventDestroy(e);
     if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -1335,11 +1376,11 @@ void dm_host_free(void* p) {
 
 namespace {
 
-// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else 2.  Two lanes let
-// two large calls share a GPU (measured 2x for concurrent 8 GiB objects, tools/lanes_probe.py,
-// profiles/r03/r03m_lanes.log); more gained nothing there, because a process's streams share
-// GPU_MAX_HW_QUEUES (4) hardware queues and a kernel waits behind any other kernel on its queue
-// (tools/hwq_probe.hip).
+// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else 2.  Every lane
+// runs on a hardware queue of its own (init_device), so L lanes overlap L large calls (measured:
+// 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound at 4 for pinned 8 GiB ones;
+// tools/lanes_probe.py, profiles/r03/r03w_lanes.log).  The default stays at 2 because a lane's
+// scratch grows to the largest object it copies and is kept.
 int default_lanes() {
     const char* v = std::getenv("DEOSS_LANES");
     const int n = v ? std::atoi(v) : 2;

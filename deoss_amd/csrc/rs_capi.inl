@@ -107,9 +107,7 @@ namespace {
 // pick_device (the caller's CallLock(..., kReserved) releases it).
 int rs_lane(dm_ctx* c) {
     std::lock_guard<std::mutex> lk(c->route_mu);
-    const int g = pick_lane_of(c, 0);
-    c->slots[g].load++;
-    return g;
+    return choose_lane(c, 0, 0);
 }
 
 // The rs scratch of the lane d belongs to (d is one of r->c->devs, on the first GPU).

@@ -1,8 +1,8 @@
-"""Concurrent large calls on ONE GPU: do they overlap?  T threads each hash the same host object
-through dm_root_buffer on one context whose device list is the box's GPU V times
-(DEOSS_VIRTUAL_DEVICES=V: V call lanes, each with its own streams, scratch and lock).  With V = 1
-every call holds the device's one lane and the calls run back to back; with V >= T each call gets
-its own lane and the leaf chains of different calls can share the chip (an 8 GiB object at 32 MiB
+"""Concurrent large calls on ONE GPU: do they overlap?  T threads each hash the same object (host
+memory through dm_root_buffer, or device memory through dm_root_device_async on the thread's own
+stream) on one context with V call lanes (dm_create_lanes: each lane its own streams, scratch and
+lock).  With V = 1 every call holds the GPU's one lane and the calls run back to back; with V >= T
+each call gets its own lane and the leaf chains of different calls can share the chip (an 8 GiB object at 32 MiB
 chunks uses 32 of the 256 CUs).  Prints one JSON line per (workload, V, T) with the wall time of
 all T calls and whether every root matched the single-call root.
 
@@ -25,14 +25,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", default="1,2,4")
     ap.add_argument("--lanes", default="1,2,4")
-    ap.add_argument("--workloads", default="pinned8g,pageable2g,pinned1m")
+    ap.add_argument("--workloads", default="device8g,pinned8g,pageable2g,pinned1m")
     ap.add_argument("--fp-gib", type=float, default=1.0, help="FullProcessing file size (0: skip)")
     args = ap.parse_args()
     import torch
     from deoss_amd import MerkleContext
     torch.cuda.init()
     gib = 1 << 30
-    shapes = {   # name -> (bytes, chunk, pinned)
+    shapes = {   # name -> (bytes, chunk, pinned); pinned None: device-resident (each thread its own stream)
+        "device8g": (8 * gib, 32 << 20, None),
         "pinned8g": (8 * gib, 32 << 20, True),
         "pageable2g": (2 * gib, 32 << 20, False),
         "pinned1m": (1 * gib, 1 << 20, True),
@@ -41,24 +42,36 @@ def main():
     lanes = [int(x) for x in args.lanes.split(",")]
     for name in filter(None, args.workloads.split(",")):
         length, chunk, pinned = shapes[name]
-        host = torch.empty(length, dtype=torch.uint8, pin_memory=pinned)
         dev = torch.empty(length, dtype=torch.uint8, device="cuda")
         with MerkleContext() as c0:
             c0.fill_synthetic_async(dev.data_ptr(), 0, length, 0xC0FFEE, 0)
             torch.cuda.synchronize()
-            host.copy_(dev)
-            del dev
-            torch.cuda.empty_cache()
-            want = c0.root_buffer_ptr(host.data_ptr(), length, chunk)[1]
+            if pinned is None:
+                host = dev
+                r0 = torch.zeros(32, dtype=torch.uint8, device="cuda")
+                c0.root_device_async(dev.data_ptr(), length, chunk, r0.data_ptr(), 0, 0)
+                torch.cuda.synchronize()
+                want = bytes(r0.cpu().numpy())
+            else:
+                host = torch.empty(length, dtype=torch.uint8, pin_memory=pinned)
+                host.copy_(dev)
+                del dev
+                torch.cuda.empty_cache()
+                want = c0.root_buffer_ptr(host.data_ptr(), length, chunk)[1]
+        streams = [torch.cuda.Stream() for _ in range(max(threads))]
+        roots_dev = torch.zeros(32 * max(threads), dtype=torch.uint8, device="cuda")
+
+        def one_call(c, i):
+            if pinned is not None:
+                return c.root_buffer_ptr(host.data_ptr(), length, chunk)[1]
+            c.root_device_async(host.data_ptr(), length, chunk, roots_dev.data_ptr() + 32 * i, 0,
+                                streams[i].cuda_stream)
+            streams[i].synchronize()
+            return bytes(roots_dev[32 * i:32 * i + 32].cpu().numpy())
         for V in lanes:
-            if V > 1:
-                os.environ["DEOSS_VIRTUAL_DEVICES"] = str(V)
-            try:
-                ctx = MerkleContext()
-            finally:
-                os.environ.pop("DEOSS_VIRTUAL_DEVICES", None)
+            ctx = MerkleContext(lanes=V)
             with ctx:
-                ctx.root_buffer_ptr(host.data_ptr(), length, chunk)   # warm lane 0
+                one_call(ctx, 0)   # warm lane 0
                 for T in threads:
                     roots = [None] * T
                     ms = [0.0] * T
@@ -67,7 +80,7 @@ def main():
                     def work(i):
                         go.wait()
                         t0 = time.perf_counter()
-                        roots[i] = ctx.root_buffer_ptr(host.data_ptr(), length, chunk)[1]
+                        roots[i] = one_call(ctx, i)
                         ms[i] = (time.perf_counter() - t0) * 1e3
 
                     for _rep in range(2):   # the first round grows every lane's scratch
