@@ -42,6 +42,7 @@ constexpr uint64_t kAlign = 256;                    // leaf start alignment when
 constexpr uint64_t kStageBytes = 64ull << 20;       // pinned staging slot
 constexpr uint64_t kStripeBudget = 256ull << 20;    // bytes per H2D stripe / batch (e2e path)
 constexpr int kMaxLanes = 8;                        // call lanes per GPU (dm_create_lanes)
+constexpr uint64_t kLaneKeepBytes = 16ull << 30;    // object buffer a lane keeps between calls (a batcher batch fits)
 
 uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
 uint64_t round_up(uint64_t a, uint64_t b) { return ceil_div(a, b) * b; }
@@ -205,6 +206,7 @@ struct Dev {
     // kernels outlive its lock, so routing counts a lane whose tail has not completed as busy
     hipEvent_t ev_tail = nullptr;
     hipStream_t tail_stream = nullptr;  // set by begin_call, recorded into ev_tail at unlock
+    uint64_t keep_bytes = kLaneKeepBytes;   // object buffer kept between calls (test hook: DEOSS_LANE_KEEP_BYTES)
     // timing records: (K1 begin, K1 end, call end) per timed call, reused across resets
     std::vector<hipEvent_t> tev;
     size_t ntimed = 0;
@@ -320,12 +322,19 @@ struct DeviceRestore {
 };
 
 // The lane's tail: its last call's work ends with this event (begin_call set tail_stream; the
-// caller holds the lane's lock).
+// caller holds the lane's lock).  Then the lane's object buffer is trimmed: a lane keeps at most
+// kLaneKeepBytes of it between calls (a larger one goes to the reaper, whose hipFree waits for the
+// work still using it), so a context's idle HBM does not scale with its lanes x its largest object.
 void record_tail(Dev& d) {
     if (!d.tail_stream) return;
     if (hipSetDevice(d.id) == hipSuccess) (void)hipEventRecord(d.ev_tail, d.tail_stream);
     (void)hipGetLastError();
     d.tail_stream = nullptr;
+    if (d.data.cap > d.keep_bytes && d.data.rp) {
+        reaper_put(d.data.rp, d.data.dev, d.data.p, false);
+        d.data.p = nullptr;
+        d.data.cap = 0;
+    }
 }
 
 // An entry point's hold on ONE lane of its context for the whole call (that lane's scratch,
@@ -1412,8 +1421,10 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
     c->lanes = lanes;
     c->devs.resize(ids.size() * (size_t)lanes);
     c->slots.reset(new DevSlot[c->devs.size()]);
+    const char* kb = std::getenv("DEOSS_LANE_KEEP_BYTES");
     for (size_t i = 0; i < c->devs.size(); i++) {   // lane-major: lane 0 of every GPU first
         c->devs[i].id = ids[i % ids.size()];
+        if (kb) c->devs[i].keep_bytes = std::strtoull(kb, nullptr, 10);
         int rc = init_device(c, c->devs[i]);
         if (rc != DM_OK) {
             dm_destroy(c);

@@ -521,14 +521,19 @@ def test_virtual_devices_concurrent_routing(oracle_lib):
         c.close()
 
 
-def test_lanes_concurrent_calls(oracle_lib, tmp_path):
+@pytest.mark.parametrize("keep", [None, "1"])
+def test_lanes_concurrent_calls(oracle_lib, tmp_path, monkeypatch, keep):
     """Call lanes (dm_create_lanes): 4 lanes of this box's one GPU, each with its own streams,
     scratch and lock.  16 threads mix host buffers (pinned zero-copy and pageable), chunk lists,
     streams, batches, files and device-resident calls on their own torch streams; every root
-    matches the oracle.  A sharded-forced context keeps lane 0 for its sharded calls."""
+    matches the oracle.  keep = "1": every lane hands its object buffer to the reaper after each
+    call (DEOSS_LANE_KEEP_BYTES; production keeps up to 16 GiB).  A sharded-forced context keeps
+    lane 0 for its sharded calls."""
     import threading
     from deoss_amd import MerkleContext
     torch = _torch()
+    if keep:
+        monkeypatch.setenv("DEOSS_LANE_KEEP_BYTES", keep)
     c = MerkleContext(lanes=4)
     assert (c.device_count, c.lane_count) == (1, 4)
     datas = [oracle_lib.splitmix_bytes(20000 + 37 * i, 1900 + i) for i in range(12)]
