@@ -63,7 +63,10 @@ enum {
  * objects with no exchange.
  * Every GPU carries DEOSS_LANES (default 2, at most 8) call lanes: each lane has its own streams,
  * scratch and lock, so that many calls run on one GPU at once and concurrent callers (one gin
- * goroutine per upload) are not serialised behind each other's leaf chains. */
+ * goroutine per upload) are not serialised behind each other's leaf chains.  A
+ * lane's compute stream owns a hardware queue (created with a full CU mask); like every HIP stream
+ * made without hipStreamNonBlocking it orders with the legacy null stream, so a caller's stream-0
+ * work and a lane's work wait for each other (the library itself never uses stream 0). */
 int dm_create(dm_ctx **out, const int *devs, int ndev);
 /* dm_create with an explicit lane count per GPU (1..8). */
 int dm_create_lanes(dm_ctx **out, const int *devs, int ndev, int lanes);
