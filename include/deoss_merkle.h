@@ -17,12 +17,13 @@
  *    n x 32 bytes in chunk order (leaf_out may be NULL).  merkletree's duplicated last leaf
  *    for odd n is NOT written (it equals leaf n-1).
  *  - Ownership: the caller owns every buffer; nothing is retained after return.
- *  - Threading: every call holds ONE device of its context (a per-device lock) for its duration;
- *    calls on different devices of one context run in parallel, calls on one device queue.  Host-
- *    memory calls (dm_root_buffer / _chunks / _batch, dm_new_hash_tree, streams) go to the least-
- *    loaded device, or are sharded over several devices when dm_plan_route says that finishes
- *    sooner (never while other calls are in flight); device-memory calls run on the device that
- *    holds their memory; an rs (dm_rs_*, FullProcessing) lives on its context's first device.
+ *  - Threading: every call holds ONE call lane of its context (a per-lane lock; each GPU has
+ *    DEOSS_LANES lanes, see dm_create) for its duration; calls on different lanes run in parallel,
+ *    calls beyond a GPU's lanes queue.  Host-memory calls (dm_root_buffer / _chunks / _batch,
+ *    dm_new_hash_tree, streams) go to the least-loaded GPU and its least-loaded lane, or are sharded
+ *    over several GPUs when dm_plan_route says that finishes sooner (never while other calls are
+ *    in flight); device-memory calls run on a lane of the GPU that holds their memory; an rs
+ *    (dm_rs_*, FullProcessing) lives on its context's first GPU and runs on its lanes.
  *  - Every call leaves the calling thread's current HIP device as it found it (the library
  *    switches to its context's devices inside the call and switches back).
  *  - `stream` arguments are hipStream_t values passed as void*, used verbatim (NULL is HIP's
