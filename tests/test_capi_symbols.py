@@ -72,6 +72,15 @@ def test_no_gpu_fails_loudly(lib):
         Processor()
     info, fid, err = FullProcessing(__file__, "", "/nonexistent-savedir")
     assert info is None and fid == "" and isinstance(err, DeossMerkleError)
+    # the download and batch-upload mirrors too (Go: FindFragment, FullProcessingFiles)
+    from deoss_amd.process import FindFragment, FullProcessingFiles
+    data, err = FindFragment(__file__, "ab" * 32)
+    assert data is None and isinstance(err, DeossMerkleError)
+    infos, fids, errs = FullProcessingFiles([__file__, ""], "", "/nonexistent-savedir")
+    assert infos == [None, None] and fids == ["", ""]
+    assert isinstance(errs[0], DeossMerkleError) and errs[1] is None
+    h2 = ctypes.c_void_p()
+    assert lib.dm_create_lanes(ctypes.byref(h2), None, 0, 2) == -7
 
 
 def test_pkg_config_file_points_at_this_checkout(lib):
