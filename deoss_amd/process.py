@@ -35,7 +35,7 @@ from .reedsolomon import DATA_SHARDS, PAR_SHARDS, Encoder
 
 SEGMENT_SIZE = 32 << 20                       # chain.SegmentSize
 FRAGMENT_SIZE = SEGMENT_SIZE // DATA_SHARDS   # chain.FragmentSize (8 MiB; node/tracker.go:250 "96M")
-WINDOW_SEGMENTS = 8                           # segments per GPU call (256 MiB of file + 768 MiB of fragments; the Go shim bounds windows in flight by DEOSS_PROCESS_MEM_GIB)
+WINDOW_SEGMENTS = 8                           # segments per GPU call (256 MiB of file + 768 MiB of fragments; the Go shim bounds the segments in flight by DEOSS_PROCESS_MEM_GIB)
 
 
 def _write_segments() -> bool:

@@ -173,7 +173,7 @@ func NewHashTree(chunkPath []string) (*merkletree.MerkleTree, error) {
 // hashing, zero-copy from pinned memory, on the least-loaded GPU (or sharded, see above).
 const BatchLimit = 256 << 20
 
-// MaxBatchers bounds the batchers (each owns 2 worker contexts per GPU): the first MaxBatchers
+// MaxBatchers bounds the batchers (each owns 4 worker contexts per GPU): the first MaxBatchers
 // distinct chunk sizes get one; calls with any other chunk size take dm_root_buffer.  DeOSS uses
 // one chunk size (chain.SegmentSize).
 const MaxBatchers = 4
@@ -207,7 +207,7 @@ func batcherFor(chunk int) (*C.dm_batcher, error) {
 	runtime.LockOSThread() // dm_batcher_last_error is thread-local
 	defer runtime.UnlockOSThread()
 	var b *C.dm_batcher
-	// 2 worker slots per GPU, 4,096 leaves per batch, 2 ms linger
+	// 4 worker slots per GPU (the library default), 4,096 leaves per batch, 2 ms linger
 	if rc := C.dm_batcher_create(&cdevs[0], C.int(len(cdevs)), C.DM_BATCH_ROOT, C.uint64_t(chunk), 0, 0, 0, 0, 0, 2000,
 		&b); rc != C.DM_OK {
 		return nil, errors.New(C.GoString(C.dm_batcher_last_error()))

@@ -44,18 +44,22 @@ import (
 	sdkprocess "github.com/CESSProject/cess-go-sdk/core/process"
 )
 
-// windowSegments: files of up to this many segments go to the GPU in one batcher call (8 x 32 MiB
-// of file plus 8 x 12 x 8 MiB of fragments = 1 GiB of Go memory); every call in flight, across
-// all goroutines, holds one slot of the process-wide memory budget.  Larger files take
-// dm_full_processing (no Go memory for the data).
+// windowSegments: files of up to this many segments go to the GPU in one batcher call (at most
+// 8 x 32 MiB of file plus 8 x 12 x 8 MiB of fragments = 1 GiB of Go memory).  Every call in
+// flight, across all goroutines, holds its segments' share of the process-wide memory budget
+// (128 MiB per segment), so a 1 MiB upload holds 1/64 of the default budget, not a whole window,
+// and up to 64 small uploads reach the batcher together.  Larger files take dm_full_processing
+// (no Go memory for the data).
 const windowSegments = 8
 
 var (
-	once    sync.Once
-	batcher *C.dm_batcher // FullProcessing requests from every goroutine
-	initEr  error
-	slots   chan struct{} // window budget: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 1 GiB per window
-	bufs    sync.Pool     // *windowBuf, reused across calls
+	once       sync.Once
+	batcher    *C.dm_batcher // FullProcessing requests from every goroutine
+	initEr     error
+	budgetMu   sync.Mutex
+	budgetCond = sync.NewCond(&budgetMu)
+	budgetFree int                          // segments: DEOSS_PROCESS_MEM_GIB (default 8) GiB / 128 MiB
+	bufs       [windowSegments + 1]sync.Pool // *windowBuf for n segments, reused across calls
 	pipes   chan *C.dm_rs // large files: each GPU's pipeline, once per call lane of its context
 	coders  []*C.dm_rs    // the same pipelines, for streams (NewWriter picks one round robin)
 	nextW   atomic.Uint64
@@ -74,12 +78,19 @@ func gpu() error {
 		if v, err := strconv.Atoi(os.Getenv("DEOSS_PROCESS_MEM_GIB")); err == nil && v > 0 {
 			budget = v
 		}
-		slots = make(chan struct{}, budget)
 		seg, total := uint64(chain.SegmentSize), uint64(chain.DataShards+chain.ParShards)
 		frag := seg / uint64(chain.DataShards)
-		bufs.New = func() any {
-			return &windowBuf{data: make([]byte, windowSegments*seg), frags: make([]byte, windowSegments*total*frag),
-				segd: make([]byte, 32*windowSegments), fragd: make([]byte, 32*windowSegments*total)}
+		perSeg := seg + total*frag // Go bytes one segment of a window holds
+		budgetFree = int(uint64(budget) << 30 / perSeg)
+		if budgetFree < windowSegments {
+			budgetFree = windowSegments // one full window always fits
+		}
+		for n := 1; n <= windowSegments; n++ {
+			k := uint64(n)
+			bufs[n].New = func() any {
+				return &windowBuf{data: make([]byte, k*seg), frags: make([]byte, k*total*frag),
+					segd: make([]byte, 32*k), fragd: make([]byte, 32*k*total)}
+			}
 		}
 		ngpu := int(C.dm_gpu_count())
 		if ngpu <= 0 {
@@ -106,7 +117,8 @@ func gpu() error {
 			}
 			coders = append(coders, rs)
 		}
-		// every visible GPU, 2 worker slots each, 4096 leaves per batch, 2 ms linger (DESIGN.md §6.9)
+		// every visible GPU, 4 worker slots each (the library default), 4096 leaves per batch, 2 ms
+		// linger (DESIGN.md §6.9)
 		if rc := C.dm_batcher_create(nil, 0, C.DM_BATCH_PROCESS, C.uint64_t(chain.SegmentSize), C.int(chain.DataShards),
 			C.int(chain.ParShards), 0, 0, 0, 2000, &batcher); rc != C.DM_OK {
 			initEr = errors.New(C.GoString(C.dm_batcher_last_error()))
@@ -127,6 +139,23 @@ func batcherError(rc C.int) error {
 	return errors.New(C.GoString(C.dm_strerror(rc)))
 }
 
+// acquireBudget blocks until n segments of the Go memory budget are free and takes them.
+func acquireBudget(n int) {
+	budgetMu.Lock()
+	for budgetFree < n {
+		budgetCond.Wait()
+	}
+	budgetFree -= n
+	budgetMu.Unlock()
+}
+
+func releaseBudget(n int) {
+	budgetMu.Lock()
+	budgetFree += n
+	budgetMu.Unlock()
+	budgetCond.Broadcast()
+}
+
 // window is one batcher call: the whole file, nseg <= windowSegments segments.
 type window struct {
 	nseg uint64
@@ -142,7 +171,7 @@ func runWindow(f *os.File, w *window, savedir string) {
 	seg := uint64(chain.SegmentSize)
 	total := uint64(chain.DataShards + chain.ParShards)
 	frag := seg / uint64(chain.DataShards)
-	b := bufs.Get().(*windowBuf)
+	b := bufs[w.nseg].Get().(*windowBuf)
 	w.buf = b
 	data := b.data[:w.n]
 	// every byte must come from this file: a pooled buffer still holds an earlier upload's bytes,
@@ -224,12 +253,12 @@ func FullProcessing(file string, cipher string, savedir string) ([]chain.Segment
 		return fullProcessingLarge(file, savedir, nseg)
 	}
 	w := &window{nseg: nseg, n: int(size)}
-	slots <- struct{}{}
+	acquireBudget(int(nseg))
 	runWindow(f, w, savedir)
-	<-slots
+	releaseBudget(int(nseg))
 	defer func() {
 		if w.buf != nil {
-			bufs.Put(w.buf)
+			bufs[nseg].Put(w.buf)
 		}
 	}()
 	if w.err != nil {

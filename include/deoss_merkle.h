@@ -323,7 +323,7 @@ enum { DM_BATCH_ROOT = 0, DM_BATCH_PROCESS = 1 };
 /* devs / ndev: GPUs to serve from (devs NULL: every visible GPU); objects are independent, so
  * requests spread over the GPUs with no exchange.  mode ROOT: unit = chunk size (each request:
  * NewHashTreeFromBuffer); PROCESS: unit = segment size with data/parity shards (each request:
- * FullProcessing).  slots (0 = 2) worker contexts per GPU; max_leaves / max_bytes per batch
+ * FullProcessing).  slots (0 = 4) worker contexts per GPU; max_leaves / max_bytes per batch
  * (0 = 4096 leaves / 16 GiB); linger_us: how long a worker waits for more requests after the
  * first before launching (0 = at once). */
 int dm_batcher_create(const int *devs, int ndev, int mode, uint64_t unit, int data_shards, int parity_shards,
