@@ -5,16 +5,21 @@
 // object it holds locally: it runs FullProcessing(fpath, "", cacheDir) -- every 32 MiB segment
 // hashed, every fragment coded, hashed and WRITTEN to cacheDir -- scans the names for the requested
 // hash, streams that file and deletes cacheDir.  The answer needs only the fragment names, so this
-// entry point computes exactly those: the file is read window by window into pinned memory
-// (double-buffered: window w + 1 is read while the GPU codes and hashes window w), the segments are
-// RS-coded on the device, every fragment is hashed (8 MiB chains, one table-mode leaf launch per
-// window; no 32 MiB segment chains, no fid, no files), and the scan stops at the first window that
-// holds the wanted name.  The matching fragment's bytes come back in `out`.
-// Same fragments and names as dm_full_processing (oracle: oracle/process_oracle.c).
+// entry point computes exactly those.  The file is read in pieces into the rs lane's small pinned
+// slots (the FullProcessing slots, 64 MiB) and copied on the lane's copy stream into a device ring
+// of two windows; each window (>= 1 GiB, so that few windows pay the 8 MiB fragment chain) gets one
+// RS launch and one table-mode leaf launch over its fragments on the lane's compute stream (no
+// 32 MiB segment chains, no fid, no files) while the next window is read; the names come back and
+// are scanned in window order, and the call stops at the first window holding the wanted one.
+// The matching fragment's bytes come back in `out`.  Same fragments and names as
+// dm_full_processing (oracle: oracle/process_oracle.c).
 
 namespace {
 
-constexpr uint64_t kFlWindowBytes = 1ull << 30;   // file bytes per GPU pass (hides the GPU under the reads)
+constexpr uint64_t kFlWindowBytes = 1ull << 30;      // smallest window (file bytes per leaf launch)
+constexpr uint64_t kFlWindowMaxBytes = 4ull << 30;   // largest window (2 in HBM + 2x parity: 24 GiB)
+constexpr int kFlSlots = 3;                          // pinned read slots (of dm_rs's 4; the 4th holds names)
+constexpr uint64_t kFlPartBytes = 8ull << 20;        // pread size (one reader thread each)
 
 }  // namespace
 
@@ -38,26 +43,49 @@ int dm_fragment_lookup(dm_rs* r, const char* path, uint64_t segment, const uint8
         return fail(c, DM_ERR_INVALID, "dm_fragment_lookup: out holds %llu bytes, a fragment is %llu",
                     (unsigned long long)out_cap, (unsigned long long)frag);
     const uint64_t nseg = ceil_div(size, segment);
-    const uint64_t win = std::min(nseg, std::max<uint64_t>(1, env_bytes("DEOSS_FL_WINDOW_BYTES", kFlWindowBytes) / segment));
+    // window: a quarter of the file, within [kFlWindowBytes, kFlWindowMaxBytes] (test hook:
+    // DEOSS_FL_WINDOW_BYTES fixes it); slot: the FullProcessing slot size, at least one segment
+    const uint64_t want_win = std::getenv("DEOSS_FL_WINDOW_BYTES")
+                                  ? env_bytes("DEOSS_FL_WINDOW_BYTES", kFlWindowBytes)
+                                  : std::min(kFlWindowMaxBytes, std::max(kFlWindowBytes, size / 4));
+    const uint64_t win = std::min(nseg, std::max<uint64_t>(1, want_win / segment));
+    const uint64_t spd = std::min(win, std::max<uint64_t>(1, env_bytes("DEOSS_FP_SLOT_BYTES", kFpSlotBytes) / segment));
     const uint64_t nwin = ceil_div(nseg, win), per = win * (uint64_t)total;   // fragments per full window
     Dev& d = c->devs[g];
     RsLane& L = rs_ln(r, d);
-    hipStream_t s = d.stream;
+    hipStream_t s = d.stream, cp = d.copy;
     RC_TRY(begin_call(c, d, s));
-    struct SyncOnExit {   // on every return: nothing queued outlives the call (the pinned slots are reused)
-        hipStream_t s;
-        ~SyncOnExit() { (void)hipStreamSynchronize(s); }
-    } sync_on_exit{s};
-    // two of everything: pinned window slots, device segments, parity and digests (window w uses w % 2)
-    HIP_TRY(pinned_grow(c, d.id, L.fp_slot[0], win * segment));
-    HIP_TRY(pinned_grow(c, d.id, L.fp_slot[1], win * segment));
-    HIP_TRY(pinned_grow(c, d.id, L.fp_slot[2], 2 * per * 32));
+    // events: pinned slot free again, window copied, window hashed (created per call)
+    struct Events {
+        hipEvent_t slot[kFlSlots] = {}, copied[2] = {}, hashed[2] = {};
+        ~Events() {
+            for (hipEvent_t e : slot) if (e) (void)hipEventDestroy(e);
+            for (int i = 0; i < 2; i++) {
+                if (copied[i]) (void)hipEventDestroy(copied[i]);
+                if (hashed[i]) (void)hipEventDestroy(hashed[i]);
+            }
+        }
+    } ev;
+    struct SyncOnExit {   // on every return: nothing queued outlives the call (slots and buffers are reused)
+        hipStream_t a, b;
+        ~SyncOnExit() {
+            (void)hipStreamSynchronize(a);
+            (void)hipStreamSynchronize(b);
+        }
+    } sync_on_exit{s, cp};
+    for (hipEvent_t& e : ev.slot) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (int i = 0; i < 2; i++) {
+        HIP_TRY(hipEventCreateWithFlags(&ev.copied[i], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev.hashed[i], hipEventDisableTiming));
+    }
+    for (int i = 0; i < kFlSlots; i++) HIP_TRY(pinned_grow(c, d.id, L.fp_slot[i], spd * segment));
+    HIP_TRY(pinned_grow(c, d.id, L.fp_slot[kFlSlots], 2 * per * 32));
     HIP_TRY(d.data.ensure(2 * win * segment));
     HIP_TRY(L.work.ensure(2 * win * pbytes));
     HIP_TRY(d.leaves.ensure(2 * per * 32));
     uint8_t* data[2] = {d.data.u8(), d.data.u8() + win * segment};
     uint8_t* par[2] = {L.work.u8(), L.work.u8() + win * pbytes};
-    uint8_t* hdig = L.fp_slot[2].u8();
+    uint8_t* hdig = L.fp_slot[kFlSlots].u8();
     // one leaf table for both halves: fragment j of segment t of half b (data fragments are
     // segment slices, parity fragments live in the parity half)
     std::vector<uint64_t> addr(2 * per), lens(2 * per, frag);
@@ -71,7 +99,8 @@ int dm_fragment_lookup(dm_rs* r, const char* path, uint64_t segment, const uint8
     RC_TRY(upload(c, d, s, d.tab_len, lens.data(), lens.size() * 8));
     const int readers = (int)std::min<uint64_t>(64, env_bytes("DEOSS_FP_READERS", kFpReaders));
     // window w's names (in segment, fragment order) against `want`: 1 found (its bytes copied to
-    // out), 0 not in this window, -1 the copy failed
+    // out), 0 not in this window, -1 the copy failed.  Window w's half is neither re-filled nor its
+    // names overwritten before w is scanned (window w + 1 is launched, and w + 2 read, after that).
     auto scan = [&](uint64_t w) -> int {
         const uint64_t ns = std::min(win, nseg - w * win);
         const uint8_t* dg = hdig + (w % 2) * per * 32;
@@ -85,37 +114,60 @@ int dm_fragment_lookup(dm_rs* r, const char* path, uint64_t segment, const uint8
             const uint8_t* src = j < k ? data[w % 2] + t * segment + (uint64_t)j * frag
                                        : par[w % 2] + t * pbytes + (uint64_t)(j - k) * frag;
             if (!out) return 1;
-            const bool ok = hipMemcpyAsync(out, src, frag, hipMemcpyDeviceToHost, s) == hipSuccess &&
-                            hipStreamSynchronize(s) == hipSuccess;
+            // on the copy stream: the compute stream may already hold the next window's chains
+            const bool ok = hipMemcpyAsync(out, src, frag, hipMemcpyDeviceToHost, cp) == hipSuccess &&
+                            hipStreamSynchronize(cp) == hipSuccess;
             return ok ? 1 : -1;
         }
         return 0;
     };
-    hipEvent_t ev_dig[2] = {d.ev_step[0], d.ev_step[1]};
     int rc = DM_OK;
-    for (uint64_t w = 0; w < nwin && rc == DM_OK; w++) {
+    uint64_t next_scan = 0, piece = 0;
+    bool slot_used[kFlSlots] = {};
+    // scan windows [next_scan, upto) in order, waiting for each; 1 = found, -1 = error
+    auto scan_upto = [&](uint64_t upto, bool wait) -> int {
+        while (next_scan < upto) {
+            hipEvent_t e = ev.hashed[next_scan % 2];
+            if (wait) {
+                if (hipEventSynchronize(e) != hipSuccess) return -1;
+            } else if (hipEventQuery(e) != hipSuccess) {
+                (void)hipGetLastError();
+                return 0;
+            }
+            const int hit = scan(next_scan++);
+            if (hit != 0) return hit;
+        }
+        return 0;
+    };
+    int hit = 0;
+    for (uint64_t w = 0; w < nwin && hit == 0; w++) {
         const int b = (int)(w % 2);
         const uint64_t s0 = w * win, ns = std::min(win, nseg - s0);
-        // host: read window w into slot b while the GPU runs window w - 1 (slot b's last H2D, from
-        // window w - 2, finished before window w - 1's digests were scanned)
-        uint8_t* slot = L.fp_slot[b].u8();
-        std::vector<FilePart> parts;
-        for (uint64_t t = 0; t < ns; t++) {
-            const uint64_t off = (s0 + t) * segment, have = std::min(segment, size - off);
-            parts.push_back({0, off, have, slot + t * segment});
-            if (have < segment) std::memset(slot + t * segment + have, 0, segment - have);   // zero padding
-        }
-        if ((rc = read_parts(c, fs, parts, readers)) != DM_OK) break;
-        if (w > 0) {   // window w - 1's names first: stop before launching w when it holds the fragment
-            if (hipEventSynchronize(ev_dig[(w - 1) % 2]) != hipSuccess) {
-                rc = fail(c, DM_ERR_HIP, "dm_fragment_lookup: window %llu", (unsigned long long)(w - 1));
-                break;
+        // half b is free: window w - 2 was hashed and scanned before window w - 1 was launched.
+        // Read the window through the pinned slots; each piece's H2D runs while the next is read,
+        // and the GPU hashes window w - 1 meanwhile.
+        for (uint64_t p0 = 0; p0 < ns; p0 += spd, piece++) {
+            const int sl = (int)(piece % kFlSlots);
+            const uint64_t np = std::min(spd, ns - p0);
+            if (slot_used[sl]) HIP_TRY(hipEventSynchronize(ev.slot[sl]));
+            uint8_t* slot = L.fp_slot[sl].u8();
+            std::vector<FilePart> parts;
+            for (uint64_t t = 0; t < np; t++) {   // 8 MiB parts, so every reader thread has work
+                const uint64_t off = (s0 + p0 + t) * segment, have = off < size ? std::min(segment, size - off) : 0;
+                for (uint64_t q = 0; q < have; q += kFlPartBytes)
+                    parts.push_back({0, off + q, std::min(kFlPartBytes, have - q), slot + t * segment + q});
+                if (have < segment) std::memset(slot + t * segment + have, 0, segment - have);   // zero padding
             }
-            const int hit = scan(w - 1);
-            if (hit < 0) rc = fail(c, DM_ERR_HIP, "dm_fragment_lookup: fragment copy");
-            if (hit != 0) break;
+            if ((rc = read_parts(c, fs, parts, readers)) != DM_OK) return rc;
+            HIP_TRY(hipMemcpyAsync(data[b] + p0 * segment, slot, np * segment, hipMemcpyHostToDevice, cp));
+            HIP_TRY(hipEventRecord(ev.slot[sl], cp));
+            slot_used[sl] = true;
         }
-        HIP_TRY(hipMemcpyAsync(data[b], slot, ns * segment, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(ev.copied[b], cp));
+        // window w - 1's names before window w is launched: a hit there ends the call without
+        // waiting for another window's chains (a window's chain, ~0.13 s, is about its read time)
+        if ((hit = scan_upto(w, true)) != 0) break;
+        HIP_TRY(hipStreamWaitEvent(s, ev.copied[b], 0));
         dm::RsArgs a{};
         for (int j = 0; j < k; j++) a.in[j] = data[b] + (uint64_t)j * frag;
         for (int i = 0; i < m; i++) a.out[i] = par[b] + (uint64_t)i * frag;
@@ -135,13 +187,13 @@ int dm_fragment_lookup(dm_rs* r, const char* path, uint64_t segment, const uint8
         la.digests = d.leaves.u8() + b * per * 32;
         RC_TRY(launch_leaves(c, d, s, la, true, true, pick_leaf_kernel(c, d, la.nleaves)));
         HIP_TRY(hipMemcpyAsync(hdig + b * per * 32, la.digests, la.nleaves * 32, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipEventRecord(ev_dig[b], s));
-        if (w + 1 == nwin) {   // the last window: nothing left to read, wait for its names
-            HIP_TRY(hipEventSynchronize(ev_dig[b]));
-            if (scan(w) < 0) rc = fail(c, DM_ERR_HIP, "dm_fragment_lookup: fragment copy");
-        }
+        HIP_TRY(hipEventRecord(ev.hashed[b], s));
     }
-    if (hipStreamSynchronize(s) != hipSuccess && rc == DM_OK) rc = fail(c, DM_ERR_HIP, "dm_fragment_lookup: sync");
+    if (hit == 0) hit = scan_upto(nwin, true);   // the windows still in flight, in order
+    if (hit < 0) rc = fail(c, DM_ERR_HIP, "dm_fragment_lookup: waiting for or copying a window");
+    // the parity ring of a large file does not stay resident (the lane trims its object buffer
+    // itself at unlock); the reaper's free waits for the work still queued
+    if (L.work.cap > kFpKeepBytes) c->reaper.put(d.id, L.work);
     return rc;
 }
 

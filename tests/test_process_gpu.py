@@ -181,16 +181,20 @@ def test_full_processing_one_call_full_segments(ctx, oracle_lib, tmp_path, monke
     p.close()
 
 
-@pytest.mark.parametrize("window", [None, 3 * 4096, 4096])
-def test_fragment_lookup(ctx, oracle_lib, tmp_path, monkeypatch, window):
+@pytest.mark.parametrize("window,slot", [(None, None), (3 * 4096, None), (4096, None), (5 * 4096, 2 * 4096),
+                                         (None, 4096)])
+def test_fragment_lookup(ctx, oracle_lib, tmp_path, monkeypatch, window, slot):
     """dm_fragment_lookup (the download handler's one fragment, node/fileHandler.go:962-979): every
     probed name is found at the oracle's (segment, index) with the oracle's bytes -- first, middle
     parity, the zero-padded last segment's last fragment --, across window boundaries (one window,
-    3-segment windows, 1-segment windows); a repeated segment resolves to its first copy; an unknown
-    name is None; file errors keep Go's text; nothing is written next to the file."""
+    3-, 5- and 1-segment windows) and pinned-slot reuse (1- and 2-segment slots, 3 slots cycling);
+    a repeated segment resolves to its first copy; an unknown name is None; file errors keep Go's
+    text; nothing is written next to the file."""
     from oracle import splitmix64_bytes
     if window:
         monkeypatch.setenv("DEOSS_FL_WINDOW_BYTES", str(window))
+    if slot:
+        monkeypatch.setenv("DEOSS_FP_SLOT_BYTES", str(slot))
     p = _processor(ctx, 4, 8, 4096)
     data = splitmix64_bytes(10 * 4096 + 999, 0xDE0554000)
     data = data[:4096] + data[:4096] + data[4096:]   # segments 0 and 1 identical
