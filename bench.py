@@ -1165,8 +1165,8 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
             "step_ms": [round(t * 1e3, 1) for t in times],
             "leaf_kernel_avg_ms": round(k_avg, 3),
             "fragment_lookup": dict(lookup, what="dm_fragment_lookup: the one fragment the download handler serves, "
-                                    "found by name (file read in 1 GiB windows, RS + fragment hashes on the GPU, no files "
-                                    "written) instead of FullProcessing + scan"),
+                                    "found by name (file read through 64 MiB pinned slots into windows of a quarter file, RS + "
+                                    "fragment hashes on the GPU, no files written) instead of FullProcessing + scan"),
             "window_path": {"GiBps": round(length / t_win / (1 << 30), 4), "ms": round(t_win * 1e3, 1),
                             "what": "read 8 segments, dm_process_buffer, write their files from Python, repeat"},
             "host_io_floor": None if floor is None else {
