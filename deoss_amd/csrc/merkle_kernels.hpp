@@ -636,12 +636,15 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
     "v_xor_b32_dpp %[s], %[r], %[r] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"
 #define DM_QS_SIGMA "v_xor_b32_dpp %[s], %[r], %[s] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"
 #endif
-#define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN)                                                   \
+// VN's round comes from lane QP of the quad (QP = "[0,1,2,3]": every lane holds it, the generic
+// path; "[j,j,j,j]": the register path's lane j holds it, see quad_block_regs)
+#define DM_QS_STEP_Q(X4, X5, X6, X7, H, HN, VN, QP)                                             \
     DM_QS_HEAD(X4, X5, X6)                                                                       \
-    "v_sub_u32_dpp %[" X6 "], %[" VN "], %[" X6 "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t" \
+    "v_sub_u32_dpp %[" X6 "], %[" VN "], %[" X6 "] quad_perm:" QP " row_mask:0xf bank_mask:0x3\n\t" \
     DM_QS_SIGMA                                                                                  \
     "v_sub_u32_dpp %[" HN "], %[" X4 "], %[" X6 "] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"    \
     "v_add3_u32 %[" X7 "], %[s], %[f], %[" H "]\n\t"
+#define DM_QS_STEP(X4, X5, X6, X7, H, HN, VN) DM_QS_STEP_Q(X4, X5, X6, X7, H, HN, VN, "[0,1,2,3]")
 // e-triple idle next step (steps 63, 64): keep X6 (the e-triple feeds forward from it), HN only
 // matters on the a-triple
 #define DM_QS_STEP_A(X4, X5, X6, X7, H, HN)                                                     \
@@ -668,11 +671,11 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
 // between the two waves sharing a SIMD in the compact case).
 #define DM_QS_ALIGN ".p2align 3\n\t"
 #define DM_QS_ALIGN_MIS ".p2align 3\n\t.if %[mis]\n\ts_nop 0\n\t.endif\n\t"
-#define DM_QS_PROLOGUE(V) DM_QS_PROLOGUE_AT(V, DM_QS_ALIGN)
+#define DM_QS_PROLOGUE(V) DM_QS_PROLOGUE_AT(V, DM_QS_ALIGN, "[0,1,2,3]")
 // H of step 0, as if made by step -1 (X6 = P3, X4 = P1); P may have just been copied from x
-#define DM_QS_PROLOGUE_AT(V, ALIGN)                                                               \
+#define DM_QS_PROLOGUE_AT(V, ALIGN, QP)                                                           \
     "s_nop 1\n\t" ALIGN                                                                          \
-    "v_sub_u32_dpp %[d], %[" V "], %[d] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"       \
+    "v_sub_u32_dpp %[d], %[" V "], %[d] quad_perm:" QP " row_mask:0xf bank_mask:0x3\n\t"         \
     "v_sub_u32_dpp %[h], %[b], %[d] row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
 // steps 0..3: the a-triple's first two steps run on stale values; their writes to P3 and P2 are
 // replaced by b and a (a-quads only) before anything reads them
@@ -688,6 +691,22 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
 #define DM_QS_TAIL(V0, V1, V2)                                                                   \
     DM_QS_STEP("a", "b", "c", "d", "h", "g", V0) DM_QS_STEP("d", "a", "b", "c", "g", "h", V1)   \
     DM_QS_STEP("c", "d", "a", "b", "h", "g", V2) DM_QS_STEP_A("b", "c", "d", "a", "g", "h")      \
+    DM_QS_FF("x3", "d", "0x3") DM_QS_FF("x2", "c", "0x3") DM_QS_FF("x1", "b", "0x3")             \
+    DM_QS_FF("x0", "a", "0x3")                                                                   \
+    DM_QS_STEP_A("a", "b", "c", "d", "h", "g") DM_QS_STEP_END("d", "a", "b", "c", "g")           \
+    DM_QS_FF("x0", "a", "0xc") DM_QS_FF("x1", "b", "0xc") DM_QS_FF("x3", "d", "0xc")             \
+    DM_QS_FF("x2", "c", "0xc")
+// The same groups with each step's VN taken from a quad lane (quad_block_regs' register path)
+#define DM_QS_STEPS4Q(V0, Q0, V1, Q1, V2, Q2, V3, Q3)                                          \
+    DM_QS_STEP_Q("a", "b", "c", "d", "h", "g", V0, Q0) DM_QS_STEP_Q("d", "a", "b", "c", "g", "h", V1, Q1) \
+    DM_QS_STEP_Q("c", "d", "a", "b", "h", "g", V2, Q2) DM_QS_STEP_Q("b", "c", "d", "a", "g", "h", V3, Q3)
+#define DM_QS_GROUP0Q(V0, Q0, V1, Q1, V2, Q2, V3, Q3)                                          \
+    DM_QS_STEP_Q("a", "b", "c", "d", "h", "g", V0, Q0) DM_QS_RESTORE_A("d", "x3")              \
+    DM_QS_STEP_Q("d", "a", "b", "c", "g", "h", V1, Q1) DM_QS_RESTORE_A("c", "x2")              \
+    DM_QS_STEP_Q("c", "d", "a", "b", "h", "g", V2, Q2) DM_QS_STEP_Q("b", "c", "d", "a", "g", "h", V3, Q3)
+#define DM_QS_TAILQ(V0, Q0, V1, Q1, V2, Q2)                                                     \
+    DM_QS_STEP_Q("a", "b", "c", "d", "h", "g", V0, Q0) DM_QS_STEP_Q("d", "a", "b", "c", "g", "h", V1, Q1) \
+    DM_QS_STEP_Q("c", "d", "a", "b", "h", "g", V2, Q2) DM_QS_STEP_A("b", "c", "d", "a", "g", "h") \
     DM_QS_FF("x3", "d", "0x3") DM_QS_FF("x2", "c", "0x3") DM_QS_FF("x1", "b", "0x3")             \
     DM_QS_FF("x0", "a", "0x3")                                                                   \
     DM_QS_STEP_A("a", "b", "c", "d", "h", "g") DM_QS_STEP_END("d", "a", "b", "c", "g")           \
@@ -739,68 +758,61 @@ __device__ __forceinline__ void quad_block_skewed(uint32_t (&x)[4], KW kw, uint3
 constexpr int kLgkmWait0 = 0xC07F;   // s_waitcnt lgkmcnt(0), no wait on vmcnt / expcnt (gfx9 encoding)
 
 // quad_block_skewed with the block's 64 words of -(K+W) in registers: the whole block is one asm
-// statement (hipcc puts an s_nop between consecutive asm statements that share registers).
+// statement (hipcc puts an s_nop between asm statements that share registers).  The 64 words are
+// spread over the 4 lanes of a quad: lane j's K[t] holds rounds 16t + 4j .. 16t + 4j + 3, and
+// round r's step reads its word from quad lane (r mod 16) / 4 by DPP (quad_perm [j,j,j,j]), so a
+// block takes 4 ds_read_b128 per lane instead of 16 (issue slots on the chain's wave) and 16
+// VGPRs instead of 64 (generated by the loop in this comment's commit: round r -> q{r/16}{r%4}).
 template <bool MIS>
-__device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[16], uint3 sh, uint32_t msk) {
+__device__ __forceinline__ void quad_block_regs(uint32_t (&x)[4], const uint4 (&K)[4], uint3 sh, uint32_t msk) {
     uint32_t p0 = x[0], p1 = x[1], p2 = x[2], p3 = x[3], h, g, r_, f_, s_, t_;
     (void)t_;
-    asm volatile(DM_QS_PROLOGUE_AT("k0", DM_QS_ALIGN_MIS)
-                 DM_QS_GROUP0("k1", "k2", "k3", "k4")
-                 DM_QS_STEPS4V("k5", "k6", "k7", "k8")
-                 DM_QS_STEPS4V("k9", "k10", "k11", "k12")
-                 DM_QS_STEPS4V("k13", "k14", "k15", "k16")
-                 DM_QS_STEPS4V("k17", "k18", "k19", "k20")
-                 DM_QS_STEPS4V("k21", "k22", "k23", "k24")
-                 DM_QS_STEPS4V("k25", "k26", "k27", "k28")
-                 DM_QS_STEPS4V("k29", "k30", "k31", "k32")
-                 DM_QS_STEPS4V("k33", "k34", "k35", "k36")
-                 DM_QS_STEPS4V("k37", "k38", "k39", "k40")
-                 DM_QS_STEPS4V("k41", "k42", "k43", "k44")
-                 DM_QS_STEPS4V("k45", "k46", "k47", "k48")
-                 DM_QS_STEPS4V("k49", "k50", "k51", "k52")
-                 DM_QS_STEPS4V("k53", "k54", "k55", "k56")
-                 DM_QS_STEPS4V("k57", "k58", "k59", "k60")
-                 DM_QS_TAIL("k61", "k62", "k63")
+    asm volatile(DM_QS_PROLOGUE_AT("q00", DM_QS_ALIGN_MIS, "[0,0,0,0]")
+                 DM_QS_GROUP0Q("q01", "[0,0,0,0]", "q02", "[0,0,0,0]", "q03", "[0,0,0,0]", "q00", "[1,1,1,1]")
+                 DM_QS_STEPS4Q("q01", "[1,1,1,1]", "q02", "[1,1,1,1]", "q03", "[1,1,1,1]", "q00", "[2,2,2,2]")
+                 DM_QS_STEPS4Q("q01", "[2,2,2,2]", "q02", "[2,2,2,2]", "q03", "[2,2,2,2]", "q00", "[3,3,3,3]")
+                 DM_QS_STEPS4Q("q01", "[3,3,3,3]", "q02", "[3,3,3,3]", "q03", "[3,3,3,3]", "q10", "[0,0,0,0]")
+                 DM_QS_STEPS4Q("q11", "[0,0,0,0]", "q12", "[0,0,0,0]", "q13", "[0,0,0,0]", "q10", "[1,1,1,1]")
+                 DM_QS_STEPS4Q("q11", "[1,1,1,1]", "q12", "[1,1,1,1]", "q13", "[1,1,1,1]", "q10", "[2,2,2,2]")
+                 DM_QS_STEPS4Q("q11", "[2,2,2,2]", "q12", "[2,2,2,2]", "q13", "[2,2,2,2]", "q10", "[3,3,3,3]")
+                 DM_QS_STEPS4Q("q11", "[3,3,3,3]", "q12", "[3,3,3,3]", "q13", "[3,3,3,3]", "q20", "[0,0,0,0]")
+                 DM_QS_STEPS4Q("q21", "[0,0,0,0]", "q22", "[0,0,0,0]", "q23", "[0,0,0,0]", "q20", "[1,1,1,1]")
+                 DM_QS_STEPS4Q("q21", "[1,1,1,1]", "q22", "[1,1,1,1]", "q23", "[1,1,1,1]", "q20", "[2,2,2,2]")
+                 DM_QS_STEPS4Q("q21", "[2,2,2,2]", "q22", "[2,2,2,2]", "q23", "[2,2,2,2]", "q20", "[3,3,3,3]")
+                 DM_QS_STEPS4Q("q21", "[3,3,3,3]", "q22", "[3,3,3,3]", "q23", "[3,3,3,3]", "q30", "[0,0,0,0]")
+                 DM_QS_STEPS4Q("q31", "[0,0,0,0]", "q32", "[0,0,0,0]", "q33", "[0,0,0,0]", "q30", "[1,1,1,1]")
+                 DM_QS_STEPS4Q("q31", "[1,1,1,1]", "q32", "[1,1,1,1]", "q33", "[1,1,1,1]", "q30", "[2,2,2,2]")
+                 DM_QS_STEPS4Q("q31", "[2,2,2,2]", "q32", "[2,2,2,2]", "q33", "[2,2,2,2]", "q30", "[3,3,3,3]")
+                 DM_QS_TAILQ("q31", "[3,3,3,3]", "q32", "[3,3,3,3]", "q33", "[3,3,3,3]")
                  : [a] "+v"(p0), [b] "+v"(p1), [c] "+v"(p2), [d] "+v"(p3), [h] "=&v"(h), [g] "=&v"(g),
                    [x0] "+v"(x[0]), [x1] "+v"(x[1]), [x2] "+v"(x[2]), [x3] "+v"(x[3]), [r] "=&v"(r_),
                    [f] "=&v"(f_), [s] "=&v"(s_) DM_QS_XOUT
                  : [mis] "i"(MIS ? 1 : 0), [sh] "v"(sh.x), [msk] "v"(msk),
-                   [k0] "v"(K[0].x), [k1] "v"(K[0].y), [k2] "v"(K[0].z), [k3] "v"(K[0].w),
-                   [k4] "v"(K[1].x), [k5] "v"(K[1].y), [k6] "v"(K[1].z), [k7] "v"(K[1].w),
-                   [k8] "v"(K[2].x), [k9] "v"(K[2].y), [k10] "v"(K[2].z), [k11] "v"(K[2].w),
-                   [k12] "v"(K[3].x), [k13] "v"(K[3].y), [k14] "v"(K[3].z), [k15] "v"(K[3].w),
-                   [k16] "v"(K[4].x), [k17] "v"(K[4].y), [k18] "v"(K[4].z), [k19] "v"(K[4].w),
-                   [k20] "v"(K[5].x), [k21] "v"(K[5].y), [k22] "v"(K[5].z), [k23] "v"(K[5].w),
-                   [k24] "v"(K[6].x), [k25] "v"(K[6].y), [k26] "v"(K[6].z), [k27] "v"(K[6].w),
-                   [k28] "v"(K[7].x), [k29] "v"(K[7].y), [k30] "v"(K[7].z), [k31] "v"(K[7].w),
-                   [k32] "v"(K[8].x), [k33] "v"(K[8].y), [k34] "v"(K[8].z), [k35] "v"(K[8].w),
-                   [k36] "v"(K[9].x), [k37] "v"(K[9].y), [k38] "v"(K[9].z), [k39] "v"(K[9].w),
-                   [k40] "v"(K[10].x), [k41] "v"(K[10].y), [k42] "v"(K[10].z), [k43] "v"(K[10].w),
-                   [k44] "v"(K[11].x), [k45] "v"(K[11].y), [k46] "v"(K[11].z), [k47] "v"(K[11].w),
-                   [k48] "v"(K[12].x), [k49] "v"(K[12].y), [k50] "v"(K[12].z), [k51] "v"(K[12].w),
-                   [k52] "v"(K[13].x), [k53] "v"(K[13].y), [k54] "v"(K[13].z), [k55] "v"(K[13].w),
-                   [k56] "v"(K[14].x), [k57] "v"(K[14].y), [k58] "v"(K[14].z), [k59] "v"(K[14].w),
-                   [k60] "v"(K[15].x), [k61] "v"(K[15].y), [k62] "v"(K[15].z), [k63] "v"(K[15].w) DM_QS_XIN);
+                   [q00] "v"(K[0].x), [q01] "v"(K[0].y), [q02] "v"(K[0].z), [q03] "v"(K[0].w),
+                   [q10] "v"(K[1].x), [q11] "v"(K[1].y), [q12] "v"(K[1].z), [q13] "v"(K[1].w),
+                   [q20] "v"(K[2].x), [q21] "v"(K[2].y), [q22] "v"(K[2].z), [q23] "v"(K[2].w),
+                   [q30] "v"(K[3].x), [q31] "v"(K[3].y), [q32] "v"(K[3].z), [q33] "v"(K[3].w) DM_QS_XIN);
 }
 
 // One ring stage (8 blocks) when every leaf of the wave has all 8: each block's 64 K+W words go
 // to registers in one burst while the previous block runs (one s_waitcnt per block instead of
-// one per 4 rounds), and no per-block branch.
+// one per 4 rounds), and no per-block branch.  kw: this lane's column (quad lane p's groups
+// 4t + p, see quad_block_regs).
 template <int G, int ROW, bool MIS>
 __device__ __forceinline__ void quad_stage_regs(uint32_t (&x)[4], const uint4* kw, uint3 sh, uint32_t msk) {
-    uint4 A[16], B[16];
+    uint4 A[4], B[4];
 #pragma unroll
-    for (int g = 0; g < 16; g++) A[g] = kw[g * G];
+    for (int t = 0; t < 4; t++) A[t] = kw[4 * t * G];
 #pragma unroll
     for (int k = 0; k < kQuadBlocks; k += 2) {
         __builtin_amdgcn_s_waitcnt(kLgkmWait0);
 #pragma unroll
-        for (int g = 0; g < 16; g++) B[g] = kw[(k + 1) * ROW + g * G];
+        for (int t = 0; t < 4; t++) B[t] = kw[(k + 1) * ROW + 4 * t * G];
         quad_block_regs<MIS>(x, A, sh, msk);
         __builtin_amdgcn_s_waitcnt(kLgkmWait0);
         if (k + 2 < kQuadBlocks) {
 #pragma unroll
-            for (int g = 0; g < 16; g++) A[g] = kw[(k + 2) * ROW + g * G];
+            for (int t = 0; t < 4; t++) A[t] = kw[(k + 2) * ROW + 4 * t * G];
         }
         quad_block_regs<MIS>(x, B, sh, msk);
     }
@@ -889,7 +901,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         for (uint64_t it = 0; it < NI; it++) {
             const uint4* kw = col + (it % kLatRing) * 16 * G;
             if ((it + 1) * kQuadBlocks <= nb_all) {
-                quad_stage_regs<G, ROW, COMPACT>(x, kw, sh, msk);
+                quad_stage_regs<G, ROW, COMPACT>(x, kw + p * G, sh, msk);   // quad lane p's groups
             } else {
                 for (uint32_t k = 0; k < kQuadBlocks; k++) {
                     const uint4* kb = kw + k * ROW;

@@ -7,8 +7,8 @@ assembly and counts the instructions of one 64-byte block:
 * ``wide`` (K1, one lane per leaf): the loop streaming 8 x global_load_dwordx4 per two blocks;
 * ``latency`` (K1L) and ``pair`` (K1P): the consumer loop (16 ds_read_b128 of K+W per block)
   and the producer loop (16 ds_write_b128 per block);
-* ``quad`` (K1Q): the consumer's whole-stage loop (8 blocks from registers, 128 ds_read_b128)
-  and the producer loop.
+* ``quad`` (K1Q): the consumer's whole-stage loop (8 blocks from registers, 32 ds_read_b128:
+  each block's words spread over a quad's lanes) and the producer loop.
 
 ``lanes`` converts wave-instruction counts into lane-slots per leaf-block: K1 runs one lane per
 leaf; per leaf-block K1L spends one consumer + one producer lane, K1P two + two, K1Q eight
@@ -112,9 +112,12 @@ def analyse(asm: str, sym: str = K1_SYMBOL) -> dict:
 
 def analyse_split(asm: str, sym: str) -> dict:
     loops = list(_loops(_function_body(asm, sym)))
-    # K1Q runs whole ring stages (8 blocks, 128 ds_read_b128) from registers when every leaf of
-    # the wave has them: that loop is the bench path; otherwise the per-block loop (16 reads)
-    stage = _smallest(loops, lambda l: sum(x.startswith("ds_read_b128") for x in l) >= 128)
+    # K1Q runs whole ring stages (8 blocks from registers: 8 x 66 steps, each ending in one
+    # v_add3_u32; 4 ds_read_b128 per block since the words are spread over a quad's lanes) when
+    # every leaf of the wave has them: that loop is the bench path; otherwise the per-block loop
+    # (16 reads)
+    stage = _smallest(loops, lambda l: sum(x.startswith("v_add3_u32") for x in l) >= 8 * 66
+                      and sum(x.startswith("ds_read_b128") for x in l) >= 32)
     if stage is not None:
         prod = _smallest(loops, lambda l: sum(x.startswith("ds_write_b128") for x in l) >= 16)
         if prod is None:
