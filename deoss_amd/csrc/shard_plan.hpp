@@ -95,10 +95,10 @@ inline Layout plan_shards(uint64_t n, int G) {
 
 // ---- cost model of one call (milliseconds), constants measured on one MI355X ----------------
 // Per-block time of one leaf chain (8 GiB at 32 MiB chunks, DESIGN.md §4.2 / §6.2 sweep):
-// K1Q 503.6 ms / 524,289 blocks; K1P 9.4 GiB/s; K1L 8.7 GiB/s; K1 5.6 GiB/s.
+// K1Q 490.6 ms / 524,289 blocks (round 3, 4-read step); K1P 9.4 GiB/s; K1L 8.7 GiB/s; K1 5.6 GiB/s.
 inline double chain_ns_per_block(int kind) {
     switch (kind) {
-        case kQuad: return 960.0;
+        case kQuad: return 936.0;
         case kPair: return 1740.0;
         case kLatency: return 1880.0;
         default: return 2730.0;
