@@ -18,3 +18,7 @@ def test_isa_counts_match_current_build():
         for field in ("valu", "valu_slots", "total", "blocks_per_iteration"):
             assert wa[field] == wb[field], (kind, field, wa[field], wb[field])
         assert isa.chain_instructions_per_block(kind) == wb["total"] / wb["blocks_per_iteration"]
+    # K1Q's register path: a block's 64 words of -(K+W) spread over a quad's 4 lanes, so the
+    # chain's wave issues 4 ds_read_b128 per block (16 before round 3)
+    q = fresh["quad"]["consumer"]
+    assert q["lds"] == 4 * q["blocks_per_iteration"], q["lds"]
