@@ -59,8 +59,19 @@ def _function_body(asm: str, sym: str) -> list:
 def _loops(body: list):
     """Yield the instruction list of every backward-branch loop."""
     labels, insts = {}, []
+    skip = []   # .if <literal> ... .endif from inline asm (DM_QS_ALIGN_MIS): count taken arms only
     for ln in body:
         s = ln.strip()
+        m = re.match(r"^\.if\s+(\S+)", s)
+        if m:
+            skip.append(m.group(1) == "0")
+            continue
+        if s.startswith(".endif"):
+            if skip:
+                skip.pop()
+            continue
+        if any(skip):
+            continue
         m = re.match(r"^(\.LBB[0-9_]+):", s)
         if m:
             labels[m.group(1)] = len(insts)
