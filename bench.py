@@ -168,9 +168,11 @@ def main() -> None:
                     help="N=1 object line: skip the other configs / entry points measured in the same run "
                          "(other_configs), the e2e host-buffer rates and the 64 KiB / 1 MiB sweep points")
     ap.add_argument("--no-verify", action="store_true", help="N>1: skip the single-GPU root check")
+    ap.add_argument("--no-aux", action="store_true",
+                    help="fullprocessing / process_upload: only the timed flow (the PMC profiling runs)")
     ap.add_argument("--workload", default="object",
                     choices=["object", "batch", "stream", "upload", "rs", "process", "proofs", "concurrent", "files", "fullprocessing", "process_upload",
-                             "plumbing"],
+                             "plumbing", "latency", "inprocess"],
                     help="object: one object per GPU (configs[1]/[3]); batch: many device-resident objects "
                          "(configs[2]); stream: many host-resident objects through the pinned ring (configs[4]); "
                          "upload: one object fed in pieces through dm_stream (hash while receiving); "
@@ -196,7 +198,25 @@ def main() -> None:
                     help="nccl = RCCL over xGMI (production); gloo = CPU exchange (rehearsal on one GPU)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (with --dist-backend gloo)")
+    ap.add_argument("--in-process", action="store_true",
+                    help="N > 1: also run the single-process multi-GPU path (one dm_ctx over every visible GPU, "
+                         "ncclCommInitAll + ncclAllGather) from rank 0 after the per-rank legs; always on at N = 8. "
+                         "With --same-device, virtual devices stand in for the GPUs (D2D instead of RCCL)")
+    ap.add_argument("--inproc-gib", type=float, default=64.0,
+                    help="in-process leg: pinned host object (GiB) hashed sharded over every GPU")
+    ap.add_argument("--inproc-timeout", type=float, default=420.0,
+                    help="in-process leg: seconds before the watchdog gives up on it (the line is printed anyway)")
+    ap.add_argument("--inproc-devices", type=int, default=8,
+                    help="--workload inprocess on one GPU: virtual devices standing in for the GPUs")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.gpus > 1 and os.environ.get("WORLD_SIZE") in (None, ""):
+        # no launcher: start the rank processes here, before anything touches torch or the GPU
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        launch_check(args)
+        return
 
     import torch
     import torch.distributed as dist
@@ -212,12 +232,25 @@ def main() -> None:
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     gloo = args.dist_backend == "gloo"
+    wait_group = None
     if world > 1:
         if gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=device)
+        # host-only group: ranks wait on it while rank 0 runs the in-process leg (no RCCL watchdog)
+        import datetime
+        wait_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(minutes=45))
 
+    if args.workload == "latency":      # the N = 1 line's latency block alone
+        print(json.dumps({"latency": latency_block(args, torch, dev_index)}), flush=True)
+        return
+    if args.workload == "inprocess":    # the N = 8 line's in-process leg alone (one process)
+        ndev = torch.cuda.device_count()
+        args.same_device = args.same_device or ndev < 2
+        print(json.dumps({"in_process": in_process_configs(args, torch, args.inproc_devices if args.same_device
+                                                           else ndev)}), flush=True)
+        return
     runners = {"upload": run_upload, "files": run_files, "plumbing": run_plumbing, "rs": run_rs,
                "process": run_process, "proofs": run_proofs, "concurrent": run_concurrent,
                "batch": run_batch, "stream": run_batch, "fullprocessing": run_fullprocessing,
@@ -243,18 +276,119 @@ def main() -> None:
     out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
     if isinstance(out.get("parity"), dict):
         out["parity"]["pinned_by"] = PIN_MERKLE
+    if world > 1:
+        out["launch"] = launch_info(torch, dist, world, rank, local_rank, dev_index, args)
     if world == 1 and rank == 0 and not args.no_extras:
         out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
+        out["latency"] = latency_block(args, torch, dev_index)
     if ((world == 8 and not args.same_device) or (world > 1 and args.multi_configs)) and not args.no_extras \
             and not args.total_gib:
         other = multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         if rank == 0:
             out["other_configs"] = other
+    if world > 1 and (world == 8 or args.in_process) and not args.no_extras and not args.total_gib:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        dist.barrier(group=wait_group)
+        inproc, hung = None, False
+        if rank == 0:
+            inproc, hung = run_with_watchdog(lambda: in_process_configs(args, torch, world), args.inproc_timeout)
+        flag = torch.tensor([1 if hung else 0], dtype=torch.int64)
+        dist.all_reduce(flag, group=wait_group)           # doubles as the barrier
+        if rank == 0:
+            out.setdefault("other_configs", {})["in_process"] = inproc
+        if int(flag.item()):   # the leg never returned (its thread may hold GPUs): print, then every rank exits
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+def run_with_watchdog(fn, timeout_s):
+    """fn() on a daemon thread, waited for at most timeout_s: (result, False), or
+    ({"error": ...}, True) when it raised / did not return in time.  The N = 8 in-process leg runs
+    this way so that a hang in it (a first RCCL init over 8 GPUs, say) cannot cost the line."""
+    import threading
+    box = {}
+
+    def body():
+        try:
+            box["r"] = fn()
+        except Exception as e:   # reported, never fatal to the headline line
+            box["r"] = {"error": f"{type(e).__name__}: {e}"}
+
+    th = threading.Thread(target=body, daemon=True)
+    th.start()
+    th.join(timeout_s)
+    if th.is_alive():
+        return {"error": f"did not finish within {timeout_s} s (watchdog)"}, True
+    return box["r"], False
+
+
+def self_launch(n: int, argv) -> int:
+    """`--gpus N > 1` with no launcher around it (WORLD_SIZE unset): start the N rank processes
+    as a child `python -m torch.distributed.run` (one process per GPU, rendezvous on 127.0.0.1, the
+    driver's own launch line) and return its exit status.  Runs before anything imports torch, so
+    this parent never initialises HIP and never execs: the ranks are children.  They inherit
+    stdout, so rank 0's JSON line is this command's line."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ, DEOSS_BENCH_LAUNCHER="bench.py self-launch (child python -m torch.distributed.run)")
+    print(f"bench.py: WORLD_SIZE unset, launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(args) -> None:
+    """Hidden --launch-check (tests/test_bench_launch.py): the ranks meet over gloo and rank 0
+    prints who they are; nothing touches a GPU.  Proves the self-launch without one."""
+    import torch.distributed as dist
+    world = env_int("WORLD_SIZE", 1)
+    rank = env_int("RANK", 0)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = {"rank": rank, "local_rank": env_int("LOCAL_RANK", 0), "pid": os.getpid()}
+    every = [None] * world
+    if world > 1:
+        dist.all_gather_object(every, mine)
+    else:
+        every = [mine]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "gpus": args.gpus, "world_size": world, "ranks": every,
+                          "launcher": os.environ.get("DEOSS_BENCH_LAUNCHER", "external (WORLD_SIZE set)")}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def launch_info(torch, dist, world, rank, local_rank, dev_index, args):
+    """What the N > 1 run actually formed: the process group's world size and backend, the GPUs
+    each rank saw and used (device id, PCI bus, UUID), and the RCCL version torch runs."""
+    props = torch.cuda.get_device_properties(dev_index)
+    mine = {"rank": rank, "local_rank": local_rank, "device": dev_index, "pid": os.getpid(),
+            "visible_devices": torch.cuda.device_count(),
+            "pci_bus_id": getattr(props, "pci_bus_id", None), "uuid": str(getattr(props, "uuid", "")) or None,
+            "name": props.name}
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    try:
+        rccl = ".".join(str(x) for x in torch.cuda.nccl.version())
+    except Exception as e:   # reported, not fatal
+        rccl = f"unavailable ({type(e).__name__})"
+    distinct = len({(r["pci_bus_id"], r["uuid"], r["device"]) for r in every})
+    return {"world_size": dist.get_world_size(), "backend": str(dist.get_backend()),
+            "device_count": torch.cuda.device_count(), "rank_devices": every,
+            "distinct_gpus": 1 if args.same_device else distinct, "rccl_version": rccl,
+            "launcher": os.environ.get("DEOSS_BENCH_LAUNCHER", "external (WORLD_SIZE set by the caller's launcher)")}
 
 
 def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
@@ -473,6 +607,401 @@ def multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, b
     return res
 
 
+def _host_mem_available() -> int:
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith("MemAvailable:"):
+                    return int(line.split()[1]) * 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    return 0
+
+
+def _fill_host(orc, addr, nbytes, seed, threads):
+    """splitmix64 bytes [0, nbytes) of stream `seed` into host memory at addr, `threads` at once."""
+    from concurrent.futures import ThreadPoolExecutor
+    piece = 256 << 20
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda o: orc.fill_splitmix_ptr(addr + o, o, min(piece, nbytes - o), seed),
+                    range(0, nbytes, piece)))
+
+
+def _pcts(xs):
+    """p50 / p99 / min / max (ms) of a list of seconds; p99 by nearest rank (= max below 100 samples)."""
+    v = sorted(xs)
+    pick = lambda q: v[min(len(v) - 1, max(0, int(-(-q * len(v) // 1)) - 1))]   # noqa: E731
+    return {"p50_ms": round(pick(0.50) * 1e3, 3), "p99_ms": round(pick(0.99) * 1e3, 3),
+            "min_ms": round(v[0] * 1e3, 3), "max_ms": round(v[-1] * 1e3, 3), "samples": len(v)}
+
+
+def latency_block(args, torch, dev_index):
+    """Per-request latency of the calls an upload handler makes, GPU vs the serial CPU restatement
+    on the same bytes, every result checked bit-exact (N = 1 line, "latency"):
+      FullProcessing of a 1 MiB and of a 64 MiB upload -- one call per upload
+        (/root/reference/node/objectHandler.go:168, node/fileHandler.go:771): GPU dm_process_buffer
+        with every fragment back in host memory, CPU oracle/process_oracle.c, both from a pageable
+        host buffer, no files;
+      NewHashTreeFromBuffer of 1 MiB at 32 MiB chunks (one leaf);
+      NewHashTree(chunkPath) over 256 x 32 MiB files in the page cache (GPU dm_new_hash_tree; CPU
+        reads each file whole, then hashes: common/hashtree/types.go:24-38).
+    p50 / p99 over repeated single calls on an otherwise idle GPU.  Then "crossover": c requests
+    arriving at once, the GPU through the coalescing batcher (dm_batcher) vs the CPU restatement
+    on the job's CPU share (one request per core at a time, as gin runs one goroutine per upload),
+    wall time for all c: the smallest c at which the GPU finishes first."""
+    import ctypes
+    import shutil
+    import tempfile
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    import numpy as np
+    from deoss_amd import MerkleContext
+    from deoss_amd.batcher import PROCESS as B_PROCESS, ROOT as B_ROOT, Batcher
+    from deoss_amd.process import Processor
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    orc = Oracle()
+    share = cpu_share()
+    seg, chunk = 32 << 20, 32 << 20
+    out = {"gpu": "one MI355X, idle, device " + str(dev_index),
+           "cpu": f"serial restatement on 1 core ({orc.backend()} SHA-256, table GF(2^8)); crossover: {share} threads",
+           "pinned_by": {"FullProcessing": PIN_PROCESS, "hashtree": PIN_MERKLE}}
+
+    def host(nbytes, seed):
+        a = np.empty((nbytes + 7) // 8 * 8, dtype=np.uint8)
+        orc.fill_splitmix_ptr(a.ctypes.data, 0, a.size, seed)
+        return a
+
+    def timed(fn, reps):
+        fn()   # warm
+        xs, r = [], None
+        for _ in range(reps):
+            t = time.perf_counter()
+            r = fn()
+            xs.append(time.perf_counter() - t)
+        return xs, r
+
+    def entry(gx, cx, ok, **kw):
+        g, c = _pcts(gx), _pcts(cx)
+        e = {"gpu": g, "cpu_1core": c, "gpu_over_cpu_p50": round(g["p50_ms"] / c["p50_ms"], 2), "bit_exact": ok}
+        e.update(kw)
+        return e
+
+    with MerkleContext(devices=[dev_index]) as ctx:
+        proc = Processor(ctx, 4, 8, seg)
+        for name, nbytes, reps in (("FullProcessing_1MiB", 1 << 20, 12), ("FullProcessing_64MiB", 64 << 20, 6)):
+            try:
+                a = host(nbytes, SEED + 0x600 + nbytes)
+                src = (ctypes.c_char * nbytes).from_address(a.ctypes.data)
+                gx, g = timed(lambda: proc.process_buffer(src, want_frags=True), reps)
+                cx, c = timed(lambda: orc.full_processing_ptr(a.ctypes.data, nbytes, seg, 4, 8, want_frags=True,
+                                                              nthreads=1), reps)
+                out[name] = entry(gx, cx, g[0] == c[0] and g[1] == c[1] and g[2] == c[2] and g[3] == c[3],
+                                  what=f"{nbytes} B upload -> {-(-nbytes // seg)} zero-padded 32 MiB segment(s), "
+                                       "RS 4+8, every segment / fragment digest, fid, fragments back in host memory")
+            except Exception as e:
+                out[name] = {"error": f"{type(e).__name__}: {e}"}
+        try:
+            a = host(1 << 20, SEED + 0x700)
+            gx, g = timed(lambda: ctx.root_buffer_ptr(a.ctypes.data, 1 << 20, chunk)[1], 30)
+            cx, c = timed(lambda: orc.root_buffer_ptr(a.ctypes.data, 1 << 20, chunk, nthreads=1)[1], 30)
+            out["NewHashTreeFromBuffer_1MiB"] = entry(gx, cx, g == c, what="1 MiB pageable buffer, chunk 32 MiB "
+                                                      "(one leaf): H2D, one SHA-256 chain, root back")
+        except Exception as e:
+            out["NewHashTreeFromBuffer_1MiB"] = {"error": f"{type(e).__name__}: {e}"}
+        base = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > (12 << 30) else None
+        d = tempfile.mkdtemp(prefix="deoss_lat_", dir=base)
+        try:
+            size, nfiles = 32 << 20, 256
+            buf = np.empty(size, dtype=np.uint8)
+            paths = []
+            for i in range(nfiles):
+                orc.fill_splitmix_ptr(buf.ctypes.data, i * size, size, SEED)
+                pth = os.path.join(d, f"seg{i:05d}")
+                buf.tofile(pth)
+                paths.append(pth)
+
+            def cpu_files(threads):
+                chunks = []
+                for pth in paths:
+                    with open(pth, "rb") as f:
+                        chunks.append(f.read())
+                return orc.root_chunks(chunks, nthreads=threads)[1]
+
+            gx, g = timed(lambda: ctx.new_hash_tree(paths)[1], 5)
+            cx, c = timed(lambda: cpu_files(1), 3)
+            px, pc = timed(lambda: cpu_files(share), 3)
+            out["NewHashTree_256x32MiB_files"] = entry(
+                gx, cx, g == c == pc, cpu_share=dict(_pcts(px), threads=share),
+                what="256 files of 32 MiB in the page cache (= BASELINE configs[1] bytes): GPU dm_new_hash_tree; "
+                     "CPU reads each file whole, then hashes (types.go:24-38)")
+        except Exception as e:
+            out["NewHashTree_256x32MiB_files"] = {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+
+    # crossover: c simultaneous requests, GPU batcher vs the CPU share
+    def crossover(mode, nbytes, cs, unit):
+        pool_n = 64
+        a = host(pool_n * nbytes, SEED + 0x800 + mode)
+        addr = a.ctypes.data
+
+        def want(j):
+            p = addr + (j % pool_n) * nbytes
+            if mode == B_ROOT:
+                return orc.root_buffer_ptr(p, nbytes, unit, nthreads=1)[1]
+            return orc.full_processing_ptr(p, nbytes, unit, 4, 8, nthreads=1)[2]
+
+        wants = [want(j) for j in range(pool_n)]
+        b = (Batcher(B_ROOT, unit, device=dev_index, linger_us=2000) if mode == B_ROOT
+             else Batcher(B_PROCESS, unit, 4, 8, device=dev_index, linger_us=2000))
+
+        def gpu_one(j):
+            p = (addr + (j % pool_n) * nbytes, nbytes)
+            return b.root(p)[1] if mode == B_ROOT else b.process(p)[2]
+
+        def gpu_wave(c):
+            got = [None] * c
+            go = threading.Barrier(c + 1)
+
+            def th(j):
+                go.wait()
+                got[j] = gpu_one(j)
+
+            ts = [threading.Thread(target=th, args=(j,)) for j in range(c)]
+            for x in ts:
+                x.start()
+            go.wait()
+            t = time.perf_counter()
+            for x in ts:
+                x.join()
+            return time.perf_counter() - t, all(got[j] == wants[j % pool_n] for j in range(c))
+
+        rows, ok, first = [], True, None
+        try:
+            gpu_wave(max(cs))   # warm every slot's buffers at the largest wave
+            with ThreadPoolExecutor(share) as ex:
+                for c in cs:
+                    tg, good = gpu_wave(c)
+                    t = time.perf_counter()
+                    got = list(ex.map(want, range(c)))
+                    tc = time.perf_counter() - t
+                    good = good and all(got[j] == wants[j % pool_n] for j in range(c))
+                    ok = ok and good
+                    rows.append({"concurrent": c, "gpu_ms": round(tg * 1e3, 2), "cpu_ms": round(tc * 1e3, 2),
+                                 "gpu_faster": tg < tc})
+                    if first is None and tg < tc:
+                        first = c
+        finally:
+            b.close()
+        return {"rows": rows, "gpu_faster_from": first, "bit_exact": ok, "cpu_threads": share,
+                "request_bytes": nbytes}
+
+    try:
+        out["crossover_FullProcessing_1MiB"] = crossover(B_PROCESS, 1 << 20, (1, 16, 64, 256), seg)
+    except Exception as e:
+        out["crossover_FullProcessing_1MiB"] = {"error": f"{type(e).__name__}: {e}"}
+    try:
+        out["crossover_NewHashTreeFromBuffer_1MiB"] = crossover(B_ROOT, 1 << 20, (1, 64, 512, 2048), chunk)
+    except Exception as e:
+        out["crossover_NewHashTreeFromBuffer_1MiB"] = {"error": f"{type(e).__name__}: {e}"}
+    out["bit_exact"] = all(v.get("bit_exact") is True for k, v in out.items() if isinstance(v, dict) and
+                           k not in ("pinned_by",))
+    return out
+
+
+def in_process_configs(args, torch, world):
+    """The single-process multi-GPU path -- what go/hashtree gets from one dm_ctx over every GPU of
+    the node (ncclCommInitAll at dm_create, one ncclAllGather per sharded call) -- run
+    by rank 0 over every visible GPU after the per-rank legs, while the other ranks wait on a host
+    barrier.  Three legs, each checked against the CPU oracle on the same bytes:
+      sharded_object: one pinned host object (--inproc-gib, 32 MiB chunks, /root/reference
+        common/hashtree/types.go:38's tree) forced through multi_root: aligned block partition
+        (dm_plan::plan_shards), every GPU hashing its chunk range in place over PCIe, the RCCL
+        all-gather of subtree roots, final levels on device 0; exchange time measured
+        (dm_exchange_timing), leaf digests and root checked;
+      batch_by_objects: a host batch of 4,096 x 4 MiB objects split by objects over the GPUs;
+      concurrent_calls: 8 threads each making one NewHashTree-shaped call (dm_root_chunks over 64 x
+        32 MiB) on an unforced context: the GPU each landed on (dm_last_call_devices) and its wall.
+    With --same-device (one GPU) the GPUs are DEOSS_VIRTUAL_DEVICES = N stand-ins on cuda:0: the
+    same code with a D2D copy in place of RCCL (a rehearsal, not a multi-GPU result)."""
+    import ctypes
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    from deoss_amd import MerkleContext, PinnedBuffer
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle
+    orc = Oracle()
+    virtual = bool(args.same_device)
+    visible = torch.cuda.device_count()
+    ndev = world if virtual else visible
+    res = {"virtual_devices": virtual, "visible_devices": visible, "devices": ndev}
+    if ndev < 2:
+        res["skipped"] = f"{visible} visible GPU(s): nothing to shard over"
+        return res
+    chunk = 32 << 20
+    size = int(args.inproc_gib * (1 << 30)) // chunk * chunk
+    avail = _host_mem_available()
+    while size > (4 << 30) and avail and 2 * size + (16 << 30) > avail:   # leave the host room
+        size //= 2
+    size = max(chunk * 2 * ndev, size // chunk * chunk)
+    threads = max(1, min(os.cpu_count() or 1, cpu_share() * (1 if virtual else world)))
+    res.update({"object_bytes": size, "chunk": chunk, "host_mem_available": avail, "cpu_threads": threads})
+    seed = SEED + 0x500
+    t0 = time.perf_counter()
+    pin = PinnedBuffer(size)
+    _fill_host(orc, pin.ptr, size, seed, threads)
+    res["setup_s"] = round(time.perf_counter() - t0, 2)
+    L = None
+
+    def make_ctx(forced):
+        env = {"DEOSS_FORCE_SHARDED": "1"} if forced else {}
+        if virtual:
+            env["DEOSS_VIRTUAL_DEVICES"] = str(ndev)
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        try:
+            t = time.perf_counter()
+            c = MerkleContext(devices=None if virtual else list(range(ndev)))
+            return c, time.perf_counter() - t
+        finally:
+            for k, v in old.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+    try:
+        # a. one object sharded over every GPU: multi_root + the RCCL all-gather
+        ctx, t_create = make_ctx(True)
+        L = ctx._L
+        leg = {"dm_create_s": round(t_create, 3), "context_devices": ctx.device_count, "lanes": ctx.lane_count,
+               "what": "dm_root_buffer of a pinned host object, DEOSS_FORCE_SHARDED: chunk ranges over every GPU, "
+                       "ncclAllGather of the 32-byte subtree roots, final levels on device 0"}
+        try:
+            ctx.root_buffer_ptr(pin.ptr, size, chunk)            # warm: staging, communicators
+            ctx.set_timing(True)
+            walls = []
+            for _ in range(3):
+                t = time.perf_counter()
+                leaves, root = ctx.root_buffer_ptr(pin.ptr, size, chunk, want_leaves=True)
+                walls.append(time.perf_counter() - t)
+            xn, xsum, xmax, xg = ctx.exchange_timing()
+            devs, ids, lane = ctx.last_call_devices()
+            ctx.set_timing(False)
+            t = time.perf_counter()
+            want_leaves, want = orc.root_buffer_ptr(pin.ptr, size, chunk, nthreads=threads, want_leaves=True)
+            cpu_s = time.perf_counter() - t
+            from deoss_amd import plan_shards
+            plan = plan_shards(size, chunk, ctx.device_count)
+            leg.update({
+                "GiBps": round(size / (sum(walls) / len(walls)) / (1 << 30), 4),
+                "wall_ms": [round(w * 1e3, 2) for w in walls],
+                "ran_on": {"context_devices": devs, "hip_devices": ids, "lane": lane},
+                "partition": {"k": plan.k, "blocks": plan.n_blocks, "leaves": plan.n_leaves},
+                "exchange": {"calls": xn, "avg_us": round(xsum / xn, 1) if xn else None,
+                             "max_us": round(xmax, 1) if xn else None, "devices": xg,
+                             "kind": "D2D copies (virtual devices)" if virtual else "ncclAllGather (RCCL)"},
+                "cpu": {"seconds": round(cpu_s, 3), "threads": threads,
+                        "GiBps": round(size / cpu_s / (1 << 30), 4)},
+                "parity": {"root": root.hex(), "cpu_root": want.hex(), "leaves": len(leaves) // 32,
+                           "bit_exact": root == want and leaves == want_leaves, "pinned_by": PIN_MERKLE}})
+        except Exception as e:
+            leg["error"] = f"{type(e).__name__}: {e}"
+        res["sharded_object"] = leg
+
+        # b. host batch split by objects (no exchange)
+        leg = {"what": "dm_root_batch of 4 MiB objects in pinned host memory, split by objects over the GPUs"}
+        try:
+            osz = 4 << 20
+            nobj = min(4096, size // osz)
+            P = (ctypes.c_void_p * nobj)(*[pin.ptr + j * osz for j in range(nobj)])
+            Ls = (ctypes.c_uint64 * nobj)(*([osz] * nobj))
+            out = ctypes.create_string_buffer(32 * nobj)
+            ctx._check(L.dm_root_batch(ctx._h, P, Ls, nobj, chunk, out), "dm_root_batch")   # warm
+            walls = []
+            for _ in range(2):
+                t = time.perf_counter()
+                ctx._check(L.dm_root_batch(ctx._h, P, Ls, nobj, chunk, out), "dm_root_batch")
+                walls.append(time.perf_counter() - t)
+            devs, ids, lane = ctx.last_call_devices()
+            with ThreadPoolExecutor(threads) as ex:
+                wants = list(ex.map(lambda j: orc.root_buffer_ptr(pin.ptr + j * osz, osz, chunk)[1], range(nobj)))
+            got = out.raw
+            mism = sum(wants[j] != got[32 * j:32 * j + 32] for j in range(nobj))
+            leg.update({"objects": nobj, "object_bytes": osz,
+                        "GiBps": round(nobj * osz / (sum(walls) / len(walls)) / (1 << 30), 4),
+                        "wall_ms": [round(w * 1e3, 2) for w in walls],
+                        "ran_on": {"context_devices": devs, "hip_devices": ids},
+                        "parity": {"checked_objects": nobj, "mismatches": int(mism), "bit_exact": mism == 0}})
+        except Exception as e:
+            leg["error"] = f"{type(e).__name__}: {e}"
+        res["batch_by_objects"] = leg
+        ctx.close()
+
+        # c. 8 concurrent NewHashTree-shaped calls, routed by the library (unforced context)
+        ctx, t_create = make_ctx(False)
+        leg = {"dm_create_s": round(t_create, 3), "lanes": ctx.lane_count,
+               "what": "8 threads, each one dm_root_chunks over 64 x 32 MiB chunks of pinned host memory at once "
+                       "(NewHashTree's in-memory form), routed by the library"}
+        try:
+            ncall = 8
+            per = max(1, min(64, size // chunk // ncall))
+            span = per * chunk
+
+            def call(i, rec):
+                P = (ctypes.c_void_p * per)(*[pin.ptr + i * span + j * chunk for j in range(per)])
+                Ls = (ctypes.c_uint64 * per)(*([chunk] * per))
+                root = ctypes.create_string_buffer(32)
+                t = time.perf_counter()
+                ctx._check(L.dm_root_chunks(ctx._h, P, Ls, per, None, root), "dm_root_chunks")
+                w = time.perf_counter() - t
+                if rec is not None:
+                    devs, ids, lane = ctx.last_call_devices()
+                    rec[i] = {"call": i, "wall_ms": round(w * 1e3, 2), "context_devices": devs, "hip_devices": ids,
+                              "lane": lane, "root": root.raw}
+
+            for i in range(ncall):            # warm every lane's staging
+                call(i, None)
+            rec = [None] * ncall
+            go = threading.Barrier(ncall + 1)
+
+            def th_main(i):
+                go.wait()
+                call(i, rec)
+
+            ths = [threading.Thread(target=th_main, args=(i,)) for i in range(ncall)]
+            for x in ths:
+                x.start()
+            go.wait()
+            t = time.perf_counter()
+            for x in ths:
+                x.join()
+            wall = time.perf_counter() - t
+            with ThreadPoolExecutor(min(threads, ncall)) as ex:
+                wants = list(ex.map(lambda i: orc.root_buffer_ptr(pin.ptr + i * span, span, chunk)[1], range(ncall)))
+            ok = all(r is not None and r["root"] == wants[i] for i, r in enumerate(rec))
+            for r in rec:
+                if r is not None:
+                    r.pop("root")
+            leg.update({"calls": rec, "wall_ms": round(wall * 1e3, 2), "chunks_per_call": per,
+                        "GiBps": round(ncall * span / wall / (1 << 30), 4),
+                        "gpus_used": sorted({d for r in rec if r for d in r["hip_devices"]}) if not virtual
+                        else sorted({d for r in rec if r for d in r["context_devices"]}),
+                        "parity": {"checked_calls": ncall, "bit_exact": ok}})
+        except Exception as e:
+            leg["error"] = f"{type(e).__name__}: {e}"
+        res["concurrent_calls"] = leg
+        ctx.close()
+    finally:
+        pin.free()
+    res["bit_exact"] = all(res.get(k, {}).get("parity", {}).get("bit_exact") is True
+                           for k in ("sharded_object", "batch_by_objects", "concurrent_calls"))
+    if virtual:
+        res["note"] = "rehearsal: virtual devices on one GPU (D2D gather); not a multi-GPU result"
+    return res
+
+
 def _summary(r):
     """The fields of a workload's result line worth keeping inside the headline line."""
     if not isinstance(r, dict):
@@ -494,7 +1023,8 @@ def _summary(r):
         keep["leaf_kernel"] = r["config"]["leaf_kernel"]
     rf = r.get("roofline")
     if rf:
-        keep["roofline"] = {k: rf.get(k) for k in ("kernel", "achieved", "peak", "unit", "frac", "traffic")}
+        keep["roofline"] = {k: rf.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+                                                   "traffic_source", "algorithmic_bytes_per_launch") if k in rf}
     if "cpu_baseline" in r:
         keep["cpu_baseline"] = r["cpu_baseline"]
     return keep
@@ -518,6 +1048,64 @@ def measure_read_peak(ctx, torch, buf, nbytes, sptr, stream, reps=5):
     return n / (ms * 1e-3) / 1e9, ms
 
 
+PCIE_PEAK_GBS = 64.0   # PCIe 5.0 x16, one direction, raw (about 55 GB/s measured)
+# Step-level roofline of each N = 1 extra: (profiles/<round>/extras_traffic.json key, bound, algorithmic
+# bytes one step must move on the bound's link, what they are).  Sizes are driver_extras()'s.
+EXTRA_ROOF = {
+    "configs[0]": ("configs0", "hbm", (64 << 20) + 2 * 32, "read the 64 MiB object once + 2 leaf digests"),
+    "configs[2]": ("configs2", "hbm", 4096 * (4 << 20) + 4096 * 32, "read 4,096 x 4 MiB once + one digest each"),
+    "configs[4]_per_gpu_share": ("configs4", "pcie", 12500 * (1 << 20) + 12500 * 32,
+                                 "12,500 x 1 MiB read once from pinned host memory (zero-copy K1Q over PCIe)"),
+    "files_NewHashTree": ("files", "pcie", 256 * (32 << 20), "256 x 32 MiB files: every byte H2D once"),
+    "upload_stream_1MiB_chunks": ("upload", "pcie", 8 << 30, "8 GiB pageable body: every byte H2D once"),
+    "FullProcessing": ("process", "hbm", (8 << 30) * 6,
+                       "RS reads 8 GiB, writes 16 GiB of parity; the leaf kernel re-reads all 24 GiB (unfused)"),
+    "reed_solomon_4+8": ("rs", "hbm", (8 << 30) * 3, "read 8 GiB of segments, write 16 GiB of parity"),
+    "FullProcessing_file": ("fullprocessing", "pcie", (2 << 30) * 3, "2 GiB file H2D + 4 GiB parity D2H"),
+    "FullProcessing_while_receiving": ("process_upload", "pcie", (2 << 30) * 3, "2 GiB body H2D + 4 GiB parity D2H"),
+}
+
+
+def extras_traffic():
+    """The newest profiles/<round>/extras_traffic.json (tools/profile_extras.sh), or {}."""
+    import glob
+    best = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "extras_traffic.json")))
+    if not best:
+        return {}, None
+    with open(best[-1]) as f:
+        return json.load(f).get("workloads", {}), os.path.relpath(best[-1], ROOT)
+
+
+def extra_roofline(name, r, traffic, src):
+    """Attach the step-level roofline (and the PMC traffic of one step) to extra `name`'s summary.
+    A kernel-level roofline the workload reports itself is kept under "kernel_level"."""
+    if name not in EXTRA_ROOF or not isinstance(r, dict) or not r.get("ms_per_step"):
+        return
+    key, bound, alg, what = EXTRA_ROOF[name]
+    e = traffic.get(key) or {}
+    peak = HBM_PEAK_GBS if bound == "hbm" else PCIE_PEAK_GBS
+    ach = alg / (r["ms_per_step"] * 1e-3) / 1e9
+    roof = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 6),
+            "traffic": e.get("traffic_bytes_per_step"), "algorithmic_bytes_per_step": alg, "what": what,
+            "time_basis": "ms_per_step (the whole step, wall clock)",
+            "traffic_scope": (f"{src}[{key}]: memory-side bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE) of every kernel one "
+                              "step launches; host-memory reads by the zero-copy kernels count too") if e else
+                             "not profiled"}
+    if e:
+        roof["traffic_over_algorithmic"] = round(e["traffic_bytes_per_step"] / alg, 4)
+        roof["traffic_kernels"] = {k: round(v["read_bytes"] + v["write_bytes"]) for k, v in e["kernels"].items()}
+    if isinstance(r.get("roofline"), dict):
+        kl = dict(r["roofline"])
+        if kl.get("traffic") is None and e:   # the kernel-level line's own kernel, from the same passes
+            leaf = [k for k in e["kernels"] if k.startswith("leaf_kernel")]
+            if len(leaf) == 1:
+                kv = e["kernels"][leaf[0]]
+                kl["traffic"] = (kv["read_bytes"] + kv["write_bytes"]) / max(kv["launches"], 1)
+                kl["traffic_source"] = f"{src}[{key}].kernels.{leaf[0]} (per launch)"
+        roof["kernel_level"] = kl
+    r["roofline"] = roof
+
+
 def driver_extras(args, torch, dist, device, dev_index):
     """N = 1 only: the other BASELINE configs and entry points, measured in the same run as the
     headline so the round's driver records them (each is also its own --workload).  A failing
@@ -528,18 +1116,18 @@ def driver_extras(args, torch, dist, device, dev_index):
         ("configs[2]", run_batch, dict(workload="batch", objects=4096, object_mib=4.0, steps=3, warmup=1)),
         ("configs[4]_per_gpu_share", run_batch, dict(workload="stream", objects=12500, object_mib=1.0, steps=2,
                                                      warmup=1)),
-        ("files_NewHashTree", run_files, dict(workload="files", objects=256, object_mib=32.0, steps=2, warmup=1,
-                                              no_cpu=True)),
+        ("files_NewHashTree", run_files, dict(workload="files", objects=256, object_mib=32.0, steps=2, warmup=1)),
         ("upload_stream_1MiB_chunks", run_upload, dict(workload="upload", chunk=1 << 20, object_gib=8.0, steps=2,
                                                        warmup=1)),
-        ("FullProcessing", run_process, dict(workload="process", object_gib=8.0, steps=2, warmup=1, no_cpu=True)),
-        ("reed_solomon_4+8", run_rs, dict(workload="rs", object_gib=8.0, steps=3, warmup=1, no_cpu=True)),
+        ("FullProcessing", run_process, dict(workload="process", object_gib=8.0, steps=2, warmup=1)),
+        ("reed_solomon_4+8", run_rs, dict(workload="rs", object_gib=8.0, steps=3, warmup=1)),
         ("FullProcessing_file", run_fullprocessing, dict(workload="fullprocessing", object_gib=2.0, steps=2,
-                                                         warmup=1, no_cpu=True)),
+                                                         warmup=1)),
         ("FullProcessing_while_receiving", run_process_upload, dict(workload="process_upload", object_gib=2.0,
                                                                     piece_kib=1024, steps=2, warmup=1)),
     ]
     res = {}
+    traffic, tsrc = extras_traffic()
     for name, fn, kw in specs:
         ns = copy.copy(args)
         ns.__dict__.update(kw)
@@ -547,6 +1135,7 @@ def driver_extras(args, torch, dist, device, dev_index):
         try:
             r = _summary(fn(ns, torch, dist, 1, 0, device, dev_index, False))
             r["pinned_by"] = pinning_for(ns.workload, getattr(ns, "mode", "root"))
+            extra_roofline(name, r, traffic, tsrc)
         except Exception as e:   # reported, never fatal to the headline line
             r = {"error": f"{type(e).__name__}: {e}"}
         r["wall_s"] = round(time.perf_counter() - t0, 2)
@@ -620,6 +1209,55 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
     return res
 
 
+def cpu_fp_baseline(orc, addr, length, seg, what, serial_segs=2, par_segs=64):
+    """cpu_baseline of the FullProcessing restatement (oracle/process_oracle.c: SHA-NI SHA-256 +
+    table GF(2^8) RS, segment after segment like the SDK) over the first segments of the same
+    bytes: 1 thread on `serial_segs`, and the job's CPU share on `par_segs` (one segment per thread
+    at a time: how a host with more cores runs concurrent uploads)."""
+    from concurrent.futures import ThreadPoolExecutor
+    nseg = max(1, -(-length // seg))
+    n1, np_ = min(nseg, serial_segs), min(nseg, par_segs)
+    b1 = min(length, n1 * seg)
+    t = time.perf_counter()
+    orc.full_processing_ptr(addr, b1, seg, 4, 8, nthreads=1)
+    serial = b1 / (time.perf_counter() - t) / (1 << 30)
+    share = cpu_share()
+    bp = min(length, np_ * seg)
+
+    def one(s_i):
+        return orc.full_processing_ptr(addr + s_i * seg, min(seg, length - s_i * seg), seg, 4, 8, nthreads=1)[2]
+
+    t = time.perf_counter()
+    with ThreadPoolExecutor(share) as ex:
+        list(ex.map(one, range(np_)))
+    par = bp / (time.perf_counter() - t) / (1 << 30)
+    return {"value": round(serial, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n1} segment(s) ({b1} B) of {what} through oracle/process_oracle.c (SHA-256 + RS 4+8 "
+                      "+ fid, serial like the SDK; in memory, no file writes)",
+            "parallel": {"value": round(par, 4), "cores": share,
+                         "sample": f"{np_} segments ({bp} B), one per thread at a time"}}
+
+
+def cpu_root_baseline(orc, addr, length, chunk, what, serial_bytes, par_s=None, par_bytes=None):
+    """cpu_baseline of the hashtree restatement (oracle/merkle_oracle.c, SHA-NI): 1 thread over the
+    first serial_bytes (whole chunks) of the same bytes, and the job's CPU share over all of them
+    (par_s: the seconds a parity check already spent doing exactly that, else timed here)."""
+    share = cpu_share()
+    b1 = max(chunk, min(length, serial_bytes) // chunk * chunk) if length > chunk else length
+    t = time.perf_counter()
+    orc.root_buffer_ptr(addr, b1, chunk, nthreads=1)
+    serial = b1 / (time.perf_counter() - t) / (1 << 30)
+    if par_s is None:
+        t = time.perf_counter()
+        orc.root_buffer_ptr(addr, length, chunk, nthreads=share)
+        par_s, par_bytes = time.perf_counter() - t, length
+    return {"value": round(serial, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{b1} B of {what}, chunk {chunk}: serial leaves then tree (oracle/merkle_oracle.c, SHA-NI; "
+                      "stands in for Go common/hashtree)",
+            "parallel": {"value": round(par_bytes / par_s / (1 << 30), 4), "cores": share,
+                         "sample": f"{par_bytes} B, leaves across threads"}}
+
+
 def golden_case(name):
     with open(os.path.join(ROOT, "tests", "golden", "merkle_golden.json")) as f:
         return next(c for c in json.load(f)["cases"] if c["name"] == name)
@@ -690,10 +1328,29 @@ def run_files(args, torch, dist, world, rank, device, dev_index, gloo):
                     chunks.append(f.read())
             orc.root_chunks(chunks, nthreads=1)
             dt = time.perf_counter() - t0
+            del chunks
+            # every file on the job's CPU share: threads read the files into one buffer, then hash
+            import numpy as np
+            from concurrent.futures import ThreadPoolExecutor
+            share = cpu_share()
+            big = np.empty(total, dtype=np.uint8)
+
+            def rd(i):
+                with open(paths[i], "rb") as f:
+                    f.readinto(memoryview(big)[i * size:(i + 1) * size])
+
+            t0 = time.perf_counter()
+            with ThreadPoolExecutor(share) as ex:
+                list(ex.map(rd, range(nfiles)))
+            _, proot = orc.root_buffer_ptr(big.ctypes.data, total, size, nthreads=share)
+            dtp = time.perf_counter() - t0
+            del big
             out["cpu_baseline"] = {"value": round(len(sample) * size / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
                                    "kind": "port", "sample": f"{len(sample)} of the same files: read whole (io.ReadAll), "
-                                   "then serial SHA-256 leaves + tree (oracle/merkle_oracle.c, SHA-NI)"}
-            del chunks
+                                   "then serial SHA-256 leaves + tree (oracle/merkle_oracle.c, SHA-NI)",
+                                   "parallel": {"value": round(total / dtp / (1 << 30), 4), "cores": share,
+                                                "sample": f"all {nfiles} files read by {share} threads, leaves across "
+                                                          "them", "bit_exact": proot == root}}
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -734,6 +1391,7 @@ def run_plumbing(args, torch, dist, world, rank, device, dev_index, gloo):
                    "chunk": chunk},
         "cpu": {"kind": "port", "cores": 1, "seconds": round(cpu_s, 4),
                 "what": "oracle/merkle_oracle.c faithful serial restatement (SHA-NI), stands in for Go common/hashtree"},
+        "cpu_baseline": cpu_root_baseline(orc, host.data_ptr(), length, chunk, "the configs[0] object", length),
         "gpu": {"device_resident_GiBps": round(length * args.steps / elapsed / (1 << 30), 4),
                 "ms_per_root": round(elapsed / args.steps * 1e3, 3), "leaf_kernel": ctx.leaf_kernel_for(2)},
         "parity": {"fixture_root": case["root"], "cpu_root": cpu_root.hex(), "gpu_root": gpu_root,
@@ -776,7 +1434,9 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         root, t, tail = one()
         times.append(t)
         tails.append(tail)
+    t0 = time.perf_counter()
     _, want = orc.root_buffer_ptr(base, length, chunk, nthreads=cpu_share())
+    par_s = time.perf_counter() - t0
     tavg = sum(times) / len(times)
     out = {
         "metric": "host-buffer upload GiB/s hashed to Merkle root while receiving (dm_stream, pageable pieces)",
@@ -789,6 +1449,9 @@ def run_upload(args, torch, dist, world, rank, device, dev_index, gloo):
         "write_ms": round((tavg - sum(tails) / len(tails)) * 1e3, 3),
         "parity": {"root": root.hex(), "cpu_root": want.hex(), "bit_exact": root == want},
     }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_root_baseline(orc, base, length, chunk, "the same upload body", 1 << 30,
+                                                par_s, length)
     return out
 
 
@@ -1005,14 +1668,7 @@ def run_process(args, torch, dist, world, rank, device, dev_index, gloo):
                    "fragment_digests_checked_segments": sorted({0, nseg - 1}), "bit_exact": bool(parity_ok)},
     }
     if world == 1 and not args.no_cpu:
-        sample = min(nseg, 2)
-        buf = host[:sample * seg].tobytes()
-        t0 = time.perf_counter()
-        orc.full_processing(buf, seg, k, m, nthreads=1)
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": round(sample * seg / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
-                               "kind": "port", "sample": f"{sample} segments x {seg} B of the same object through "
-                               "oracle/process_oracle.c (SHA-NI SHA-256 + table GF(2^8) RS, serial like the SDK)"}
+        out["cpu_baseline"] = cpu_fp_baseline(orc, host.ctypes.data, length, seg, "the same object")
     return out
 
 
@@ -1098,6 +1754,10 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
         # the download handler's question (node/fileHandler.go:962-979): one fragment by its name.
         # dm_fragment_lookup vs the FullProcessing call the handler makes for it; bytes checked
         # against the fragment file FullProcessing just wrote
+        if args.no_aux:   # profiling run (tools/profile_extras.sh): the timed calls' kernels only
+            return {"metric": "FullProcessing(file) (profiling run, --no-aux)",
+                    "value": round(length / tavg / (1 << 30), 4), "unit": "GiB/s", "ms_per_step": round(tavg * 1e3, 3),
+                    "parity": parity}
         lookup = {}
         for tag, t_idx in [("last_fragment", nseg * total - 1), ("first_segment_parity", k)]:
             name = fragd[32 * t_idx:32 * t_idx + 32].hex()
@@ -1180,14 +1840,9 @@ def run_fullprocessing(args, torch, dist, world, rank, device, dev_index, gloo):
             "parity": parity,
         }
         if not args.no_cpu:
-            sample_n = min(nseg, 2)
-            buf = open(path, "rb").read(sample_n * seg)
-            t0 = time.perf_counter()
-            orc.full_processing(buf, seg, k, m, nthreads=1)
-            dt = time.perf_counter() - t0
-            out["cpu_baseline"] = {"value": round(len(buf) / dt / (1 << 30), 4), "unit": "GiB/s", "cores": 1,
-                                   "kind": "port", "sample": f"{sample_n} segments of the same file through "
-                                   "oracle/process_oracle.c (SHA-256 + RS, serial like the SDK; no file writes)"}
+            host = np.fromfile(path, dtype=np.uint8, count=min(length, 64 * seg))
+            out["cpu_baseline"] = cpu_fp_baseline(orc, host.ctypes.data, host.size, seg, "the same file")
+            del host
         return out
     finally:
         shutil.rmtree(d, ignore_errors=True)
@@ -1263,7 +1918,7 @@ def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
             return t1 - t0, t1 - t_last, fid.hex(), (segd, fragd)
 
         res = {}
-        for name, fn in (("streamed", streamed), ("after", after)):
+        for name, fn in (("streamed", streamed),) + ((("after", after),) if not args.no_aux else ()):
             for _ in range(args.warmup):
                 fresh()
                 fn()
@@ -1272,6 +1927,11 @@ def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
                 fresh()
                 runs.append(fn())
             res[name] = runs
+        if args.no_aux:   # profiling run (tools/profile_extras.sh): the streamed flow's kernels only
+            tot = sum(r[0] for r in res["streamed"]) / len(res["streamed"])
+            return {"metric": "upload body through the streamed handler flow (profiling run, --no-aux)",
+                    "value": round(length / tot / (1 << 30), 4), "unit": "GiB/s", "ms_per_step": round(tot * 1e3, 1),
+                    "fid": res["streamed"][-1][2]}
         # the same flows with the body arriving at a network link's rate (2 GiB at 1.25 GB/s = 10 GbE)
         link, link_bytes = 1.25e9, min(length, 2 << 30)
         for name, fn in (("streamed_10GbE", streamed), ("after_10GbE", after)):
@@ -1307,7 +1967,8 @@ def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
             tot = sum(r[0] for r in runs) / len(runs)
             return {"GiBps": round(link_bytes / tot / (1 << 30), 4), "ms": round(tot * 1e3, 1),
                     "tail_ms_after_last_piece": round(sum(r[1] for r in runs) / len(runs) * 1e3, 1)}
-        return {
+        cpu = cpu_fp_baseline(orc, addr, length, seg, "the same upload body") if not args.no_cpu else None
+        res_line = {
             "metric": "GiB/s of upload body through the handler flow: body -> file + FullProcessing (fid, fragment files)",
             "value": sv["GiBps"], "unit": "GiB/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": sv["ms"], "higher_is_better": True, "scaling": "none", "vs_baseline": None,
@@ -1321,6 +1982,9 @@ def run_process_upload(args, torch, dist, world, rank, device, dev_index, gloo):
                          "streamed": summ_link(res["streamed_10GbE"]), "after_file_saved": summ_link(res["after_10GbE"])},
             "parity": parity,
         }
+        if cpu:
+            res_line["cpu_baseline"] = cpu
+        return res_line
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -1599,8 +2263,15 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
     def want_root(j):
         return orc.root_buffer_ptr(base + j * pitch, obj, chunk, nthreads=1)[1]
 
+    t0 = time.perf_counter()
     with ThreadPoolExecutor(cpu_share()) as pool:
         wants = list(pool.map(want_root, range(nobj)))
+    par_s = time.perf_counter() - t0
+    ns = min(nobj, 64)
+    t0 = time.perf_counter()
+    for j in range(ns):
+        want_root(j)
+    ser_s = time.perf_counter() - t0
     check = nobj
     mism = sum(wants[j] != got[32 * j:32 * j + 32] for j in range(nobj)) + gen_bad
     leaves = (obj + chunk - 1) // chunk * nobj
@@ -1622,6 +2293,10 @@ def run_batch(args, torch, dist, world, rank, device, dev_index, gloo):
         "k1_avg_ms": round(k1_ms_sum / max(ncalls, 1), 4), "call_avg_ms": round(call_ms_sum / max(ncalls, 1), 4),
         "parity": {"checked_objects": check, "objects": nobj, "mismatches": int(mism), "bit_exact": mism == 0,
                    "generator_sample_checked": gen_checked},
+        "cpu_baseline": {"value": round(ns * obj / ser_s / (1 << 30), 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+                         "sample": f"{ns} of the same objects, one after another (oracle/merkle_oracle.c, SHA-NI)",
+                         "parallel": {"value": round(total_local / par_s / (1 << 30), 4), "cores": cpu_share(),
+                                      "sample": f"all {nobj} objects of this rank, one per thread at a time"}},
     }
     if args.same_device:
         out.update({"ranks": world, "same_device": True,

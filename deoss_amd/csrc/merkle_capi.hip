@@ -55,6 +55,7 @@ uint64_t ceil_shift(uint64_t n, uint32_t k) { return k >= 64 ? (n ? 1 : 0) : (n 
 
 struct Reaper;
 void reaper_put(Reaper* r, int dev, void* p, bool pinned);
+void reaper_drain(Reaper* r);
 
 struct DevBuf {
     void* p = nullptr;
@@ -76,7 +77,19 @@ struct DevBuf {
         }
         size_t c = round_up(std::max<size_t>(n, 4096), 2ull << 20);
         hipError_t e = hipMalloc(&p, c);
-        if (e != hipSuccess) return e;
+        if (e == hipErrorOutOfMemory && rp) {
+            // the memory this growth needs may still sit in the reaper's queue (this buffer's old
+            // block among it, freed only once every stream of the device has drained): wait for
+            // those frees, then try once more
+            (void)hipGetLastError();
+            p = nullptr;
+            reaper_drain(rp);
+            e = hipMalloc(&p, c);
+        }
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
         cap = c;
         return hipSuccess;
     }
@@ -110,7 +123,7 @@ struct PinnedBuf {
 };
 
 // Deferred release.  hipFree, hipFreeAsync and hipHostFree wait for ALL work queued on the device
-// (tools/free_sync_probe.hip, profiles/r03/free_sync_probe.log: ~280 ms behind an unrelated 300 ms
+// (tools/free_sync_probe.hip, profiles/r03/LOGS.md#free_sync_probe.log: ~280 ms behind an unrelated 300 ms
 // kernel on another stream; hipMalloc and event calls do not wait).  So buffers a call no longer
 // needs go to the context's reaper thread, which frees them in order: the caller never waits for
 // other callers' kernels.  The same device-wide wait makes it safe: every use of a buffer was
@@ -125,6 +138,8 @@ struct Reaper {
     };
     std::deque<Item> q;
     bool stop = false;
+    int active = 0;                   // items popped but not yet freed
+    std::condition_variable idle;     // q empty and nothing being freed (drain)
     std::thread th;
     void put(int dev, void* p, bool pinned) {
         if (!p) return;
@@ -154,13 +169,25 @@ struct Reaper {
                 if (q.empty()) return;   // stop requested and drained
                 it = q.front();
                 q.pop_front();
+                active++;
             }
             if (hipSetDevice(it.dev) == hipSuccess) {
                 if (it.pinned) (void)hipHostFree(it.p);
                 else (void)hipFree(it.p);
             }
             (void)hipGetLastError();
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                active--;
+            }
+            idle.notify_all();
         }
+    }
+    // Block until everything queued so far has been freed (an allocation that failed for lack of
+    // memory retries after this).  The frees wait for the devices' queued work, never for a lock.
+    void drain() {
+        std::unique_lock<std::mutex> lk(mu);
+        idle.wait(lk, [&] { return q.empty() && active == 0; });
     }
     void finish() {   // free everything queued, then end the thread (dm_destroy)
         {
@@ -174,10 +201,11 @@ struct Reaper {
 };
 
 void reaper_put(Reaper* r, int dev, void* p, bool pinned) { r->put(dev, p, pinned); }
+void reaper_drain(Reaper* r) { r->drain(); }
 
 // The HIP resources of one streaming upload (dm_stream / dm_pstream), pooled per device and reused
 // by the next stream: creating streams and pinning staging costs ~10 ms per object
-// (profiles/r03/free_sync_probe.log), and destroying / unpinning waits for the whole device.
+// (profiles/r03/LOGS.md#free_sync_probe.log), and destroying / unpinning waits for the whole device.
 struct StreamKit {
     static constexpr int kEvents = 10, kSlots = 4;
     hipStream_t copy = nullptr;          // high priority: staging reuse never waits behind leaf kernels
@@ -200,8 +228,7 @@ struct Dev {
     uint64_t htab_used = 0;
     hipEvent_t ev_done = nullptr;
     hipEvent_t ev_copy[2] = {nullptr, nullptr}, ev_step[2] = {nullptr, nullptr}, ev_htab = nullptr;
-    hipStream_t last_stream = nullptr;  // stream of the last enqueued call (scratch ordering)
-    bool has_last = false;
+    bool has_last = false;              // the lane has run a call (ev_tail is recorded)
     // end of the lane's last call on the GPU (recorded when its lock is released): an async call's
     // kernels outlive its lock, so routing counts a lane whose tail has not completed as busy
     hipEvent_t ev_tail = nullptr;
@@ -249,6 +276,12 @@ struct dm_ctx {
     // compaction and the batch split run with G = N on a one-GPU box.  RCCL rejects duplicate
     // GPUs, so the gather of subtree roots is then a D2D copy to device 0 (real GPUs: RCCL).
     bool virtual_devs = false;
+    // Exchange timing of multi-device calls while timing is on (dm_exchange_timing): host clock
+    // from every device's subtree roots being ready to the gathered slots being on every device.
+    std::mutex xmu;
+    uint64_t x_n = 0;
+    double x_sum_us = 0, x_max_us = 0;
+    int x_last_G = 0;
 };
 
 namespace {
@@ -264,6 +297,24 @@ int set_err(int code, const char* msg) {
 }
 
 int bad_arg() { return set_err(DM_ERR_INVALID, "invalid argument"); }
+
+// Where the calling thread's last lane-holding call ran (dm_last_call_devices): context device
+// indices (one for a whole call, [0, G) for a call sharded over G GPUs) and the lane.
+thread_local std::vector<int> t_call_devs;
+thread_local int t_call_lane = -1;
+thread_local const dm_ctx* t_call_ctx = nullptr;
+
+void note_call(const dm_ctx* c, int g, int G) {
+    t_call_ctx = c;
+    t_call_devs.clear();
+    if (G == 1) {
+        t_call_devs.push_back(g % c->nphys);
+        t_call_lane = g / c->nphys;
+    } else {
+        for (int i = 0; i < G; i++) t_call_devs.push_back(i);
+        t_call_lane = 0;
+    }
+}
 
 int fail(dm_ctx* c, int code, const char* fmt, ...) {
     char buf[1024];
@@ -349,6 +400,7 @@ struct CallLock {
     CallLock(dm_ctx* c, int g, bool reserved = false) : d(&c->devs[g]), slot(&c->slots[g]) {
         if (!reserved) slot->load++;
         lk = std::unique_lock<std::mutex>(slot->mu);
+        note_call(c, g, 1);
     }
     ~CallLock() {
         record_tail(*d);
@@ -366,11 +418,15 @@ struct RangeLock {
     dm_ctx* c;
     int G;
     std::vector<std::unique_lock<std::mutex>> lks;
-    RangeLock(dm_ctx* c_, int G_) : c(c_), G(G_) {
+    // lanes [0, G): lane 0 of the first G GPUs, for a call sharded over them
+    RangeLock(dm_ctx* c_, int G_) : RangeLock(c_, G_, true) {}
+    // every lane: context-wide settings (not a call: dm_last_call_devices keeps the last call)
+    explicit RangeLock(dm_ctx* c_) : RangeLock(c_, (int)c_->devs.size(), false) {}
+    RangeLock(dm_ctx* c_, int G_, bool is_call) : c(c_), G(G_) {
         for (int g = 0; g < G; g++) c->slots[g].load++;
         for (int g = 0; g < G; g++) lks.emplace_back(c->slots[g].mu);
+        if (is_call) note_call(c, 0, G);
     }
-    explicit RangeLock(dm_ctx* c_) : RangeLock(c_, (int)c_->devs.size()) {}
     ~RangeLock() {
         for (int g = 0; g < G; g++) record_tail(c->devs[g]);
         for (auto& l : lks) l.unlock();
@@ -492,7 +548,13 @@ uint8_t* kit_table(dm_ctx* c, int dev, StreamKit* k, uint64_t bytes) {
 hipError_t pinned_grow(dm_ctx* c, int dev, PinnedBuf& b, uint64_t n) {
     if (n <= b.cap) return hipSuccess;
     c->reaper.put(dev, b);
-    return b.ensure(n);
+    hipError_t e = b.ensure(n);
+    if (e == hipErrorOutOfMemory) {   // the old buffer may still be queued: free it, retry once
+        (void)hipGetLastError();
+        c->reaper.drain();
+        e = b.ensure(n);
+    }
+    return e;
 }
 
 // Lane for a device-memory call (device-resident entry points run where their data lives), counted
@@ -517,11 +579,12 @@ int device_of(dm_ctx* c, const void* p) {
 // Order this call's use of the context scratch after the previous call's (possibly other stream).
 int begin_call(dm_ctx* c, Dev& d, hipStream_t s) {
     HIP_TRY(hipSetDevice(d.id));
-    // after the lane's previous call when that one ran on another stream: wait for its tail event
-    // (recorded when its lock was released), never for the old stream itself, which its caller
-    // may have destroyed since
-    if (d.has_last && d.last_stream != s) HIP_TRY(hipStreamWaitEvent(s, d.ev_tail, 0));
-    d.last_stream = s;
+    // after the lane's previous call: wait for its tail event (recorded when its lock was
+    // released), never for the old stream itself, which its caller may have destroyed since.
+    // Always, even when s compares equal to the last stream: a caller may have destroyed that
+    // stream and created a new one at the same address while the old one's kernels (which use
+    // this lane's scratch) still run; the wait is near-free on a completed event.
+    if (d.has_last) HIP_TRY(hipStreamWaitEvent(s, d.ev_tail, 0));
     d.has_last = true;
     d.tail_stream = s;
     return DM_OK;
@@ -906,7 +969,7 @@ int pack_chunks(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens
 // overlaps nothing (the GPU waits for it), and each later one must finish within the previous
 // stripe's hashing (transfers run ~1.2x the chain-bound hash rate at 256 x 32 MiB).  Offsets and
 // widths are multiples of 64 (whole blocks).  Measured on the files path: 15.45 -> 15.70 GiB/s
-// (profiles/r02/r02x_files.log).
+// (profiles/r02/LOGS.md#r02x_files.log).
 void stripe_schedule(uint64_t W, uint64_t len, std::vector<uint64_t>& so, std::vector<uint64_t>& sw) {
     so.clear();
     sw.clear();
@@ -1052,7 +1115,7 @@ int init_device(dm_ctx* c, Dev& d) {
     // before it on its queue (tools/hwq_probe.hip; tools/conc_probe.hip: 4 normal streams run side
     // by side, a 5th waits).  Which queue a lane would get then depends on every stream the process
     // made before (torch's included): measured, two lanes' 0.5 s chains shared one queue after a
-    // caller had created 4 streams (profiles/r03/r03u_lanes.log).  A stream made with a CU mask gets
+    // caller had created 4 streams (profiles/r03/LOGS.md#r03u_lanes.log).  A stream made with a CU mask gets
     // a hardware queue of its own (conc_probe cumask: 8 such streams side by side after 8 ordinary
     // ones), so each lane's compute stream is one, with every CU enabled.  Such streams synchronise
     // with the legacy null stream (the library never uses it; a caller's stream-0 work orders with
@@ -1187,6 +1250,15 @@ int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_
         }
     // C1: all-gather of fixed-size slots (maxc nodes of 32 B per device) over RCCL
     const size_t slot = maxc * 32;
+    const bool timed = c->timing;
+    std::chrono::steady_clock::time_point x0;
+    if (timed) {   // measured exchange: every device's subtree roots ready first
+        for (int g = 0; g < G; g++) {
+            HIP_TRY(hipSetDevice(c->devs[g].id));
+            HIP_TRY(hipStreamSynchronize(c->devs[g].stream));
+        }
+        x0 = std::chrono::steady_clock::now();
+    }
     if (c->virtual_devs) {   // test hook: every context device is the same GPU (no RCCL), see dm_ctx
         for (int g = 0; g < G; g++) {
             Dev& d = c->devs[g];
@@ -1201,6 +1273,18 @@ int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_
             NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream));
         }
         NCCL_TRY(ncclGroupEnd());
+    }
+    if (timed) {
+        for (int g = 0; g < G; g++) {
+            HIP_TRY(hipSetDevice(c->devs[g].id));
+            HIP_TRY(hipStreamSynchronize(c->devs[g].stream));
+        }
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - x0).count();
+        std::lock_guard<std::mutex> lk(c->xmu);
+        c->x_n++;
+        c->x_sum_us += us;
+        c->x_max_us = std::max(c->x_max_us, us);
+        c->x_last_G = G;
     }
     Dev& d0 = c->devs[0];
     HIP_TRY(hipSetDevice(d0.id));
@@ -1385,15 +1469,23 @@ void dm_host_free(void* p) {
 
 namespace {
 
-// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else 2.  Every lane
-// runs on a hardware queue of its own (init_device), so L lanes overlap L large calls (measured:
-// 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound at 4 for pinned 8 GiB ones;
-// tools/lanes_probe.py, profiles/r03/r03w_lanes.log).  The default stays at 2 because a lane's
-// scratch grows to the largest object it copies and is kept.
-int default_lanes() {
+// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else sized from the
+// first GPU's free HBM.  Every lane runs on a hardware queue of its own (init_device), so L lanes
+// overlap L large calls (measured: 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound
+// at 4 for pinned 8 GiB ones; tools/lanes_probe.py, profiles/r03/LOGS.md#r03w_lanes.log).  What a lane
+// costs while idle is the object buffer it keeps between calls, at most kLaneKeepBytes (16 GiB),
+// so the default is as many lanes (up to 4) as keep at most half of the free HBM idle: 4 on an
+// MI355X (288 GB), fewer on a GPU with little free memory.
+int default_lanes(int dev) {
     const char* v = std::getenv("DEOSS_LANES");
-    const int n = v ? std::atoi(v) : 2;
-    return std::min(std::max(n, 1), kMaxLanes);
+    if (v && *v) return std::min(std::max(std::atoi(v), 1), kMaxLanes);
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return 2;
+    }
+    const uint64_t by_hbm = (uint64_t)free_b / (2 * kLaneKeepBytes);
+    return (int)std::min<uint64_t>(std::max<uint64_t>(by_hbm, 1), 4);
 }
 
 int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
@@ -1450,7 +1542,14 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
 
 extern "C" {
 
-int dm_create(dm_ctx** out, const int* devs, int ndev) { return ctx_create(out, devs, ndev, default_lanes()); }
+int dm_create(dm_ctx** out, const int* devs, int ndev) {
+    int first = (devs && ndev > 0) ? devs[0] : 0;
+    int count = 0;
+    DeviceRestore dr;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return set_err(DM_ERR_NODEV, "no usable GPU");
+    if (first < 0 || first >= count) return bad_arg();
+    return ctx_create(out, devs, ndev, default_lanes(first));
+}
 
 int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) { return ctx_create(out, devs, ndev, lanes); }
 
@@ -1486,7 +1585,36 @@ int dm_set_timing(dm_ctx* ctx, int enable) {
     RangeLock lk(ctx);
     ctx->timing = enable != 0;
     for (auto& d : ctx->devs) d.ntimed = 0;
+    std::lock_guard<std::mutex> xl(ctx->xmu);
+    ctx->x_n = 0;
+    ctx->x_sum_us = ctx->x_max_us = 0;
+    ctx->x_last_G = 0;
     return DM_OK;
+}
+
+int dm_exchange_timing(dm_ctx* ctx, uint64_t* n, double* us_sum, double* us_max, int* last_ndev) {
+    if (!ctx) return bad_arg();
+    std::lock_guard<std::mutex> xl(ctx->xmu);
+    if (n) *n = ctx->x_n;
+    if (us_sum) *us_sum = ctx->x_sum_us;
+    if (us_max) *us_max = ctx->x_max_us;
+    if (last_ndev) *last_ndev = ctx->x_last_G;
+    return DM_OK;
+}
+
+int dm_last_call_devices(dm_ctx* ctx, int* devs, int* hip_ids, int cap, int* lane) {
+    if (!ctx || cap < 0) return bad_arg();
+    if (t_call_ctx != ctx) {   // no call of this context on this thread yet
+        if (lane) *lane = -1;
+        return 0;
+    }
+    const int n = (int)t_call_devs.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        if (devs) devs[i] = t_call_devs[i];
+        if (hip_ids) hip_ids[i] = ctx->devs[t_call_devs[i]].id;
+    }
+    if (lane) *lane = t_call_lane;
+    return n;
 }
 
 int dm_timing_summary(dm_ctx* ctx, uint64_t* ncalls, double* leaf_ms_sum, double* total_ms_sum, double* leaf_ms_max) {

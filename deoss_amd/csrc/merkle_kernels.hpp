@@ -1036,7 +1036,7 @@ __global__ __launch_bounds__(kBlock) void fill_splitmix_kernel(uint64_t* dst, ui
 // HBM read-bandwidth probe (the measured read peak bench.py reports next to the 8 TB/s spec,
 // SURVEY.md 8d): XOR of every 8-byte word of [p, p + 16 * n16).  Each workgroup streams one
 // contiguous slab with 16 nontemporal 16-byte loads in flight per lane.  Measured A/B over 8 GiB
-// (tools/read_peak_ab.hip, profiles/r02/r02o_read_ab2.log): grid-stride with 4 loads 5.3 TB/s,
+// (tools/read_peak_ab.hip, profiles/r02/LOGS.md#r02o_read_ab2.log): grid-stride with 4 loads 5.3 TB/s,
 // slabs 5.7, slabs with nontemporal loads 6.7 TB/s.  One global atomic XOR per workgroup; *out
 // must be zero before the launch.
 constexpr int kProbeLoads = 16;

@@ -237,7 +237,10 @@ int dm_rs_create(dm_ctx* ctx, int data_shards, int parity_shards, dm_rs** out) {
         }
     hipError_t e = hipSetDevice(d.id);
     if (e == hipSuccess) e = r->enc_tab.ensure(tab.size() * 8);
-    if (e == hipSuccess) e = hipMemcpy(r->enc_tab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
+    // on the first lane's copy stream (non-blocking), not hipMemcpy's null stream: that one would
+    // wait for every lane's queued chains on this GPU (their compute streams order with it)
+    if (e == hipSuccess) e = hipMemcpyAsync(r->enc_tab.p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, d.copy);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.copy);
     if (e != hipSuccess) {
         r->enc_tab.release();
         delete r;

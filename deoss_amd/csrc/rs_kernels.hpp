@@ -13,7 +13,7 @@
 // A lane owns 16 consecutive positions (one uint4 per shard), so per 16 positions it issues nin
 // 16-B loads, 16*nin ds_read_b64, and nout 16-B stores; the position-major accumulators are
 // turned into shard-major output words by 4x4 byte transposes (v_perm_b32).
-// What bounds it (tools/rs_ab.hip, profiles/r02/r02d_rs_ab_repeats.log, interleaved repeats on one
+// What bounds it (tools/rs_ab.hip, profiles/r02/LOGS.md#r02d_rs_ab_repeats.log, interleaved repeats on one
 // box): this kernel 5.09 ms per 8 GiB of segments, the same access pattern with no table at all
 // 5.13 ms, a conflict-free variant (replicated nibble tables, 0 bank conflicts) 5.23 ms.  The
 // random-index bank conflicts (68 % of LDS cycles) are hidden under the 1-read : 2-write HBM

@@ -128,7 +128,7 @@ inline double feed_bytes_per_s(int src) {
 constexpr double kHostBytesPerS = 500e9;   // 2-socket DDR5 host (~1.2 TB/s peak), PCIe reads + copies
 // Fixed cost of a sharded call: a host thread per device, per-device setup, the gather of the
 // 32-byte nodes and the final levels on the first device.  Measured with G virtual devices on one
-// GPU (tools/shard_overhead.py, profiles/r03/shard_overhead.log: +0.093 / 0.230 / 0.463 ms at
+// GPU (tools/shard_overhead.py, profiles/r03/LOGS.md#shard_overhead.log: +0.093 / 0.230 / 0.463 ms at
 // G = 2 / 4 / 8 over one device, i.e. ~0.06 ms per device), plus 0.1 ms for the RCCL all-gather
 // of a few KiB over xGMI that a one-GPU box cannot measure (an estimate).
 inline double shard_overhead_ms(int G) { return G > 1 ? 0.10 + 0.06 * G : 0.0; }

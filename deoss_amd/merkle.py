@@ -18,7 +18,8 @@ from ._lib import DM_ERR_EMPTY, DeossMerkleError, load_library
 
 class MerkleContext:
     def __init__(self, devices: Optional[Sequence[int]] = None, lanes: Optional[int] = None):
-        """``lanes``: call lanes per GPU (``dm_create_lanes``); None = ``DEOSS_LANES`` or 2."""
+        """``lanes``: call lanes per GPU (``dm_create_lanes``); None = ``DEOSS_LANES``, else sized
+        from free HBM (4 on an MI355X)."""
         self._L = load_library()
         h = ctypes.c_void_p()
         arr = (ctypes.c_int * len(devices))(*devices) if devices else None
@@ -298,6 +299,28 @@ class MerkleContext:
         self._check(self._L.dm_timing_summary(self._h, ctypes.byref(n), ctypes.byref(a), ctypes.byref(b),
                                               ctypes.byref(m)), "dm_timing_summary")
         return n.value, a.value, b.value, m.value
+
+    def exchange_timing(self) -> Tuple[int, float, float, int]:
+        """(sharded calls, sum of exchange us, max exchange us, G of the last one) since
+        set_timing(True): the subtree-root all-gather (C1) of each sharded call."""
+        n = ctypes.c_uint64()
+        a, m = ctypes.c_double(), ctypes.c_double()
+        g = ctypes.c_int()
+        self._check(self._L.dm_exchange_timing(self._h, ctypes.byref(n), ctypes.byref(a), ctypes.byref(m),
+                                               ctypes.byref(g)), "dm_exchange_timing")
+        return n.value, a.value, m.value, g.value
+
+    def last_call_devices(self) -> Tuple[List[int], List[int], int]:
+        """Where this thread's last call on the context ran: (context device indices, HIP device
+        ids, lane); ([], [], -1) before the first call."""
+        cap = max(self.device_count, 1)
+        devs, ids = (ctypes.c_int * cap)(), (ctypes.c_int * cap)()
+        lane = ctypes.c_int()
+        n = self._L.dm_last_call_devices(self._h, devs, ids, cap, ctypes.byref(lane))
+        if n < 0:
+            self._check(n, "dm_last_call_devices")
+        n = min(n, cap)
+        return list(devs[:n]), list(ids[:n]), lane.value
 
 
 class MerkleStream:

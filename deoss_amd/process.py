@@ -368,6 +368,14 @@ def FindFragment(fpath: str, fragment_hash: str) -> Tuple[Optional[bytes], Optio
     """process.FindFragment (go/process/process_hip.go) on the default GPU pipeline: the fragment
     of ``fpath`` named ``fragment_hash``, or (None, None) when the file has no such fragment."""
     global _default
+    # file names are lower-case hex SHA-256 (node/fileHandler.go:968): any other spelling names no
+    # fragment, as the handler's string comparison would find none
+    try:
+        ok = len(fragment_hash) == 64 and bytes.fromhex(fragment_hash).hex() == fragment_hash
+    except ValueError:
+        ok = False
+    if not ok:
+        return None, None
     try:
         if _default is None:
             _default = Processor()

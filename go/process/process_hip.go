@@ -368,9 +368,12 @@ func fullProcessingLarge(file, savedir string, nseg uint64) ([]chain.SegmentData
 // Returns (nil, nil) when no fragment of the file has that name, as the handler's scan falls
 // through to the chain.  The first match in (segment, index) order wins, as in the handler.
 func FindFragment(fpath, fragmentHash string) ([]byte, error) {
+	// The handler compares fragmentHash with file names, which are lower-case hex SHA-256
+	// (node/fileHandler.go:968): any other spelling (upper case, wrong length, not hex) names no
+	// fragment, so it is not found -- never decoded into a digest that would match one.
 	want, err := hex.DecodeString(fragmentHash)
-	if err != nil || len(want) != 32 {
-		return nil, errors.New("invalid fragment hash")
+	if err != nil || len(want) != 32 || hex.EncodeToString(want) != fragmentHash {
+		return nil, nil
 	}
 	if err := gpu(); err != nil {
 		return nil, err

@@ -62,7 +62,8 @@ enum {
  * shards it: a single object is then split by aligned chunk ranges across devices [0, G') and the
  * per-device subtree roots are gathered with RCCL ("C1"); a batch is split by
  * objects with no exchange.
- * Every GPU carries DEOSS_LANES (default 2, at most 8) call lanes: each lane has its own streams,
+ * Every GPU carries DEOSS_LANES call lanes (at most 8; unset: as many, up to 4, as keep at most half
+ * of the first GPU's free HBM in idle lane buffers of <= 16 GiB each: 4 on an MI355X), each with its own streams,
  * scratch and lock, so that many calls run on one GPU at once and concurrent callers (one gin
  * goroutine per upload) are not serialised behind each other's leaf chains.  A
  * lane's compute stream owns a hardware queue (created with a full CU mask); like every HIP stream
@@ -378,6 +379,17 @@ int dm_set_timing(dm_ctx *ctx, int enable);
  * sum of whole-call durations (ms), longest K1 duration (ms). */
 int dm_timing_summary(dm_ctx *ctx, uint64_t *ncalls, double *leaf_ms_sum, double *total_ms_sum,
                       double *leaf_ms_max);
+/* Subtree-root exchanges (C1) of sharded calls since dm_set_timing(ctx, 1): their number, the sum
+ * and maximum of their durations in microseconds (host clock, from every device's level-k nodes
+ * being ready to the gathered slots being on every device: the ncclAllGather over G GPUs; while
+ * timing is on the call waits for the subtree roots before the gather) and the G of the last one. */
+int dm_exchange_timing(dm_ctx *ctx, uint64_t *n, double *us_sum, double *us_max, int *last_ndev);
+/* Where the calling thread's last call on ctx ran (any entry point that holds a lane): the context
+ * device indices (devs: one for a whole call, 0 .. G-1 for a call sharded over G GPUs) and their
+ * HIP device ids (hip_ids), at most cap entries each (both nullable), and the lane within the GPU
+ * (*lane, nullable; -1 when this thread has made no call on ctx).  Returns the device count, 0 when
+ * there was no call.  Lets a gateway log which GPU served an upload. */
+int dm_last_call_devices(dm_ctx *ctx, int *devs, int *hip_ids, int cap, int *lane);
 
 #ifdef __cplusplus
 }

@@ -136,17 +136,17 @@ inline Result FullProcessing(const std::string& file, const std::string& cipher,
 // of that name, or an error.  dm_fragment_lookup: nothing is written to disk.
 inline std::pair<std::vector<uint8_t>, std::optional<Error>> FindFragment(const std::string& fpath,
                                                                           const std::string& fragment_hash) {
+    // fragment files are named by lower-case hex SHA-256 and the handler compares strings
+    // (node/fileHandler.go:968): any other spelling names no fragment (not found, no error)
     uint8_t want[32];
-    auto nib = [](char ch) -> int {
-        return ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : ch >= 'A' && ch <= 'F' ? ch - 'A' + 10 : -1;
-    };
+    auto nib = [](char ch) -> int { return ch >= '0' && ch <= '9' ? ch - '0' : ch >= 'a' && ch <= 'f' ? ch - 'a' + 10 : -1; };
     bool ok = fragment_hash.size() == 64;
     for (int i = 0; ok && i < 32; i++) {
         const int hi = nib(fragment_hash[2 * i]), lo = nib(fragment_hash[2 * i + 1]);
         ok = hi >= 0 && lo >= 0;
         want[i] = (uint8_t)(hi * 16 + lo);
     }
-    if (!ok) return {{}, Error{DM_ERR_INVALID, "invalid fragment hash"}};
+    if (!ok) return {{}, std::nullopt};
     auto& p = Pipelines::instance();
     dm_rs* rs = p.pick();
     if (!rs) return {{}, Error{p.status(), dm_strerror(p.status())}};

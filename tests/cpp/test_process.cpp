@@ -2,6 +2,7 @@
 // file and the streaming Writer, both against the CPU oracle's restatement of the SDK composition
 // (oracle/process_oracle.c, linked in only as the checker).  Prints "PASS" and exits 0 on success.
 #include <cstdio>
+#include <cctype>
 #include <cstring>
 #include <fstream>
 #include <iterator>
@@ -67,8 +68,15 @@ int main(int argc, char** argv) {
     {
         auto [none, nerr] = process::FindFragment(file, std::string(64, 'a'));
         EXPECT(!nerr && none.empty());
-        auto [bad, berr] = process::FindFragment(file, "xyz");
-        EXPECT(berr.has_value());
+        auto [bad, berr] = process::FindFragment(file, "xyz");   // names no fragment: not found, no error
+        EXPECT(!berr && bad.empty());
+        const std::string upper = [&] {
+            std::string u = process::hex32(wf.data() + 32);
+            for (char& ch : u) ch = (char)std::toupper((unsigned char)ch);
+            return u;
+        }();
+        auto [up, uerr] = process::FindFragment(file, upper);     // the lower-case name exists; this spelling does not
+        EXPECT(!uerr && up.empty());
     }
 
     // Writer: io.MultiWriter(f, w) in the handler; pieces of 1 B .. 5 MiB

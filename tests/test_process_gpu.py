@@ -239,7 +239,9 @@ def test_fragment_lookup_full_segments(ctx, oracle_lib, tmp_path, monkeypatch):
     t = 3 * 12 + 7
     assert proc.FindFragment(str(f), frag_b[32 * t:32 * t + 32].hex()) == (frags[t * fr:(t + 1) * fr], None)
     assert proc.FindFragment(str(f), "cd" * 32) == (None, None)
-    assert proc.FindFragment(str(f), "zz")[1] is not None
+    # names are lower-case hex (node/fileHandler.go:968 compares strings): other spellings find nothing
+    assert proc.FindFragment(str(f), "zz") == (None, None)
+    assert proc.FindFragment(str(f), frag_b[32 * t:32 * t + 32].hex().upper()) == (None, None)
 
 
 def test_full_processing_files_batch_upload(oracle_lib, tmp_path):

@@ -106,7 +106,7 @@ __global__ __launch_bounds__(256) void stream12_kernel(dm::RsArgs a) {
 // Conflict-free alternative measured against the shipped kernel: nibble tables (T[x] =
 // T[x & 15] ^ T[x & 0xf0], GF(2^8) products are xor-linear), 32 bank-pair replicas interleaved so
 // lane l reads only banks 2(l%32), 2(l%32)+1.  Bit-identical output; 0 bank conflicts, 2.4x the
-// VALU, and 2.7 % slower (profiles/r02/r02d_rs_ab_repeats.log): not shipped.
+// VALU, and 2.7 % slower (profiles/r02/LOGS.md#r02d_rs_ab_repeats.log): not shipped.
 constexpr int kNib = 32;
 template <int NIN>
 __global__ __launch_bounds__(256) void rs_nib_kernel(dm::RsArgs a) {
