@@ -741,9 +741,15 @@ def latency_block(args, torch, dev_index):
             shutil.rmtree(d, ignore_errors=True)
 
     # crossover: c simultaneous requests, GPU batcher vs the CPU share
-    def crossover(mode, nbytes, cs, unit):
+    def crossover(mode, nbytes, cs, unit, pinned=False):
         pool_n = 64
         a = host(pool_n * nbytes, SEED + 0x800 + mode)
+        pin = None
+        if pinned:   # request bodies in page-locked memory (Go: hashtree.NewPinnedBuffer)
+            from deoss_amd import PinnedBuffer
+            pin = PinnedBuffer(a.size)
+            pin.array()[:] = a
+            a = pin.array()
         addr = a.ctypes.data
 
         def want(j):
@@ -794,17 +800,22 @@ def latency_block(args, torch, dev_index):
                         first = c
         finally:
             b.close()
+            if pin is not None:
+                del a
+                pin.free()
         return {"rows": rows, "gpu_faster_from": first, "bit_exact": ok, "cpu_threads": share,
-                "request_bytes": nbytes}
+                "request_bytes": nbytes, "bodies": "pinned host memory" if pinned else "pageable host memory"}
 
     try:
         out["crossover_FullProcessing_1MiB"] = crossover(B_PROCESS, 1 << 20, (1, 16, 64, 256), seg)
     except Exception as e:
         out["crossover_FullProcessing_1MiB"] = {"error": f"{type(e).__name__}: {e}"}
-    try:
-        out["crossover_NewHashTreeFromBuffer_1MiB"] = crossover(B_ROOT, 1 << 20, (1, 64, 512, 2048), chunk)
-    except Exception as e:
-        out["crossover_NewHashTreeFromBuffer_1MiB"] = {"error": f"{type(e).__name__}: {e}"}
+    for pinned in (False, True):
+        name = "crossover_NewHashTreeFromBuffer_1MiB" + ("_pinned" if pinned else "")
+        try:
+            out[name] = crossover(B_ROOT, 1 << 20, (1, 64, 512, 2048), chunk, pinned)
+        except Exception as e:
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
     out["bit_exact"] = all(v.get("bit_exact") is True for k, v in out.items() if isinstance(v, dict) and
                            k not in ("pinned_by",))
     return out
@@ -1049,7 +1060,7 @@ def measure_read_peak(ctx, torch, buf, nbytes, sptr, stream, reps=5):
 
 
 PCIE_PEAK_GBS = 64.0   # PCIe 5.0 x16, one direction, raw (about 55 GB/s measured)
-# Step-level roofline of each N = 1 extra: (profiles/<round>/extras_traffic.json key, bound, algorithmic
+# Step-level roofline of each N = 1 extra: (profiles/extras_traffic.json key, bound, algorithmic
 # bytes one step must move on the bound's link, what they are).  Sizes are driver_extras()'s.
 EXTRA_ROOF = {
     "configs[0]": ("configs0", "hbm", (64 << 20) + 2 * 32, "read the 64 MiB object once + 2 leaf digests"),
@@ -1067,13 +1078,13 @@ EXTRA_ROOF = {
 
 
 def extras_traffic():
-    """The newest profiles/<round>/extras_traffic.json (tools/profile_extras.sh), or {}."""
-    import glob
-    best = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "extras_traffic.json")))
-    if not best:
+    """profiles/extras_traffic.json (tools/profile_extras.sh: PMC passes over one step of each
+    extra, this round's code), or {}."""
+    path = os.path.join(ROOT, "profiles", "extras_traffic.json")
+    if not os.path.exists(path):
         return {}, None
-    with open(best[-1]) as f:
-        return json.load(f).get("workloads", {}), os.path.relpath(best[-1], ROOT)
+    with open(path) as f:
+        return json.load(f).get("workloads", {}), "profiles/extras_traffic.json"
 
 
 def extra_roofline(name, r, traffic, src):

@@ -217,7 +217,7 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
     // default 4 slots per GPU: each slot's context has its own hardware queue (a CU-masked lane
     // stream), so 4 batches run side by side; measured 2 / 3 / 4 / 6 / 8 slots: 0.278 / 0.370 /
     // 0.400 / 0.398 / 0.402 GiB/s of 1 MiB FullProcessing uploads, roots 8.2 (2) / 9.1 (4) / 8.4 (8)
-    // GiB/s (profiles/r03/r03y_*.log, r03z_*.log)
+    // GiB/s (profiles/r03/LOGS.md (r03y_*.log), r03z_*.log)
     const int per = slots ? slots : 4;
     const int ns = per * (int)dl.size();
     for (int i = 0; i < ns; i++) {   // slot i on device dl[i % ndev]: consecutive slots alternate GPUs

@@ -215,7 +215,7 @@ int files_leaves(dm_ctx* c, Dev& d, const FileSet& fs, uint64_t l0, uint64_t l1)
     // striped: file i's bytes [j*W, (j+1)*W) arrive in step j.  Copy mode: row i of the HBM image
     // has pitch P.  Zero-copy mode (auto, latency regime: zero_copy_regime): K1Q reads each stripe
     // straight out of the pinned staging slot it was pread into, no H2D copy and no HBM image
-    // (profiles/r02/r02v_*.log); a slot is refilled once the launch that read it has finished.
+    // (profiles/r02/LOGS.md (r02v_*.log)); a slot is refilled once the launch that read it has finished.
     const uint64_t W = std::max<uint64_t>(64, (kStripeBudget / n) / 64 * 64);
     std::vector<uint64_t> so, sw;   // ramped stripes (stripe_schedule)
     stripe_schedule(W, maxlen, so, sw);

@@ -203,6 +203,104 @@ struct Reaper {
 void reaper_put(Reaper* r, int dev, void* p, bool pinned) { r->put(dev, p, pinned); }
 void reaper_drain(Reaper* r) { r->drain(); }
 
+// Host copies into the pinned staging ring, spread over a few threads.  One thread's memcpy from
+// pageable memory into pinned memory runs well below PCIe (the ring's H2D side), so a pageable
+// source was copy-bound (1 MiB requests through the batcher: ~13 GiB/s).  One process-wide pool
+// (DEOSS_COPY_THREADS helpers, default 7; 0 = the caller alone) serves every lane: a call splits
+// its copies into pieces of at most kCopyPiece and copies them together with the helpers, pulling
+// pieces from a shared index, so concurrent calls share the helpers and the caller always makes
+// progress itself.
+constexpr size_t kCopyPiece = 4ull << 20;
+struct CopyItem {
+    void* dst;
+    const void* src;
+    size_t n;
+};
+class CopyPool {
+  public:
+    static CopyPool& get() {
+        static CopyPool pool;
+        return pool;
+    }
+    void run(const std::vector<CopyItem>& items) {
+        size_t total = 0;
+        for (const CopyItem& it : items) total += it.n;
+        if (total == 0) return;
+        auto job = std::make_shared<Job>();
+        for (const CopyItem& it : items)
+            for (size_t o = 0; o < it.n; o += kCopyPiece)
+                job->pieces.push_back({static_cast<uint8_t*>(it.dst) + o, static_cast<const uint8_t*>(it.src) + o,
+                                       std::min(kCopyPiece, it.n - o)});
+        const size_t helpers = std::min(nthreads_, job->pieces.size() - 1);
+        if (helpers) {
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                for (size_t h = 0; h < helpers; h++) q_.push_back(job);
+            }
+            if (helpers == 1) cv_.notify_one();
+            else cv_.notify_all();
+        }
+        work(*job);
+        std::unique_lock<std::mutex> lk(job->mu);
+        job->cv.wait(lk, [&] { return job->done == job->pieces.size(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+
+  private:
+    struct Job {
+        std::vector<CopyItem> pieces;
+        std::atomic<size_t> next{0};
+        size_t done = 0;   // guarded by mu
+        std::mutex mu;
+        std::condition_variable cv;
+    };
+    static void work(Job& j) {
+        size_t mine = 0;
+        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size(); mine++) {
+            const CopyItem& p = j.pieces[i];
+            std::memcpy(p.dst, p.src, p.n);
+        }
+        if (mine) {
+            std::lock_guard<std::mutex> lk(j.mu);
+            j.done += mine;
+            if (j.done == j.pieces.size()) j.cv.notify_all();
+        }
+    }
+    CopyPool() {
+        const char* v = std::getenv("DEOSS_COPY_THREADS");
+        nthreads_ = v && *v ? (size_t)std::max(0, std::atoi(v)) : 7;
+        for (size_t t = 0; t < nthreads_; t++)
+            th_.emplace_back([this] {
+                for (;;) {
+                    std::shared_ptr<Job> j;
+                    {
+                        std::unique_lock<std::mutex> lk(mu_);
+                        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+                        if (q_.empty()) return;
+                        j = q_.front();
+                        q_.pop_front();
+                    }
+                    work(*j);
+                }
+            });
+    }
+    size_t nthreads_ = 0;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<Job>> q_;
+    std::vector<std::thread> th_;
+    bool stop_ = false;
+};
+
+void par_copy(const std::vector<CopyItem>& items) { CopyPool::get().run(items); }
+
 // The HIP resources of one streaming upload (dm_stream / dm_pstream), pooled per device and reused
 // by the next stream: creating streams and pinning staging costs ~10 ms per object
 // (profiles/r03/LOGS.md#free_sync_probe.log), and destroying / unpinning waits for the whole device.
@@ -876,7 +974,7 @@ bool pinned_view(const void* const* ptrs, const uint64_t* lens, uint64_t n, std:
 // Zero-copy: leaves in pinned host memory are read in place by K1Q over PCIe, without a copy
 // to HBM.  K1Q's producer lanes load 8 consecutive 64-byte blocks per leaf, so its reads cross
 // PCIe as whole lines.  Measured from torch-pinned memory (tools/zero_copy_diag.py,
-// profiles/r02/r02s_zc_*.log), zero-copy vs copy: 8 GiB as 256 x 32 MiB 15.81 vs 15.63 GiB/s (the
+// profiles/r02/LOGS.md (r02s_zc_*.log)), zero-copy vs copy: 8 GiB as 256 x 32 MiB 15.81 vs 15.63 GiB/s (the
 // chain rate either way, without the 8 GiB device copy), 8,192 x 1 MiB 53.2 vs 52.4 (PCIe),
 // batches of 1 MiB objects 51.5 vs 43.8 (4,096), 53.2 vs 46.9 (8,192), 49.4 vs 47.6 (12,500).
 // K1L, K1P and K1 reach only ~41 GB/s reading host memory (tools/zero_copy_probe.py), so the
@@ -920,8 +1018,11 @@ int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uin
     int slot = 0;
     bool busy[2] = {false, false};
     uint64_t fill = 0, slot_dev_off = 0;
+    std::vector<CopyItem> pending;   // this slot's host copies, done together at flush (par_copy)
     auto flush = [&]() -> int {
         if (fill == 0) return DM_OK;
+        par_copy(pending);   // while the other slot's H2D is in flight
+        pending.clear();
         HIP_TRY(hipMemcpyAsync(d.data.u8() + slot_dev_off, d.stage[slot].p, fill, hipMemcpyHostToDevice, d.copy));
         HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
         busy[slot] = true;
@@ -940,7 +1041,7 @@ int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uin
         }
         if (fill != 0 && (off[i] != slot_dev_off + fill || fill + span > kStageBytes)) RC_TRY(flush());
         if (fill == 0) slot_dev_off = off[i];
-        if (lens[i]) std::memcpy(d.stage[slot].u8() + fill, ptrs[i], lens[i]);
+        if (lens[i]) pending.push_back({d.stage[slot].u8() + fill, ptrs[i], (size_t)lens[i]});
         fill += span;
     }
     RC_TRY(flush());
@@ -1027,7 +1128,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
                                        hipMemcpyHostToDevice, d.copy));
             } else {
                 if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
-                std::memcpy(d.stage[slot].p, static_cast<const uint8_t*>(host) + o, sz);
+                par_copy({{d.stage[slot].p, static_cast<const uint8_t*>(host) + o, (size_t)sz}});
                 HIP_TRY(hipMemcpyAsync(d.data.u8() + o, d.stage[slot].p, sz, hipMemcpyHostToDevice, d.copy));
                 HIP_TRY(hipEventRecord(d.ev_copy[slot], d.copy));
                 busy[slot] = true;
@@ -1068,8 +1169,11 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         } else {
             if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
             uint8_t* st = d.stage[slot].u8();
-            for (uint64_t r = 0; r + 1 < n; r++) std::memcpy(st + r * w, src + r * chunk + b0, w);
-            if (last_w) std::memcpy(st + (n - 1) * w, src + (n - 1) * chunk + b0, last_w);
+            std::vector<CopyItem> rows;
+            rows.reserve(n);
+            for (uint64_t r = 0; r + 1 < n; r++) rows.push_back({st + r * w, src + r * chunk + b0, (size_t)w});
+            if (last_w) rows.push_back({st + (n - 1) * w, src + (n - 1) * chunk + b0, (size_t)last_w});
+            par_copy(rows);
             if (n > 1)
                 HIP_TRY(hipMemcpy2DAsync(d.data.u8() + b0, chunk, st, w, w, n - 1, hipMemcpyHostToDevice, d.copy));
             if (last_w)

@@ -30,6 +30,11 @@
  *    null stream, e.g. torch's default stream).  *_async calls only enqueue work on that
  *    stream; device inputs must be ready in stream order and outputs are valid once the
  *    stream has reached that point.  Synchronous calls use the context's own streams.
+ *    Cost of NULL: the null (legacy default) stream orders with every blocking stream of its GPU,
+ *    and each lane's compute stream is one (dm_create), so an *_async call on NULL starts only
+ *    after the chains other lanes have queued on that GPU (up to ~0.5 s at 32 MiB chunks), and
+ *    their later work waits for it.  Pass a stream created with hipStreamNonBlocking (torch's
+ *    side streams are) to run beside them.  The library itself never uses the null stream.
  *  - Tree rule (merkletree v0.2.0, restated in DESIGN.md): level out[j] = SHA256(in[2j] ||
  *    in[min(2j+1, n-1)]), repeated until one node remains, at least one level (n = 1 gives
  *    SHA256(leaf || leaf)).

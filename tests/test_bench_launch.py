@@ -68,3 +68,17 @@ def test_external_launcher_is_used_as_is():
     assert r.returncode == 0, r.stderr[-3000:]
     c = json.loads(r.stdout.strip().splitlines()[-1])
     assert c["world_size"] == 1 and c["launcher"].startswith("external")
+
+
+def test_watchdog_returns_on_time_and_reports_hangs():
+    """run_with_watchdog (the N = 8 in-process leg's guard): a result, an exception and a hang."""
+    import threading
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.run_with_watchdog(lambda: {"ok": 1}, 5) == ({"ok": 1}, False)
+    r, hung = bench.run_with_watchdog(lambda: 1 / 0, 5)
+    assert not hung and r["error"].startswith("ZeroDivisionError")
+    stop = threading.Event()
+    r, hung = bench.run_with_watchdog(lambda: stop.wait(30), 0.2)
+    stop.set()
+    assert hung and "watchdog" in r["error"]

@@ -1,6 +1,6 @@
 """Sum rocprofv3 FETCH_SIZE / WRITE_SIZE passes of one-step extra workloads into per-step traffic.
 
-Usage: python tools/pmc_extras.py <gpurun_out/<tag>_pmc> <profiles/<tag>/extras_traffic.json>
+Usage: python tools/pmc_extras.py <gpurun_out/<tag>_pmc> <profiles/extras_traffic.json> [tag]
 
 Input: <dir>/<name>/{FETCH_SIZE,WRITE_SIZE}/**/*counter_collection.csv from tools/profile_extras.sh
 (each pass one `bench.py --workload ... --warmup 0 --steps 1` run).  Per workload, every kernel
@@ -42,7 +42,8 @@ def dispatches(path_glob):
 
 def main():
     src, dst = sys.argv[1], sys.argv[2]
-    res = {"source": f"{src}/<name>/{{FETCH_SIZE,WRITE_SIZE}} (rocprofv3 --pmc, separate passes, one step each)",
+    res = {"round": sys.argv[3] if len(sys.argv) > 3 else None,
+           "source": f"{src}/<name>/{{FETCH_SIZE,WRITE_SIZE}} (rocprofv3 --pmc, separate passes, one step each)",
            "correction": "bytes = FETCH_SIZE*1024*2 + WRITE_SIZE*1024 (gfx950, 16 B/lane)",
            "scope": "every kernel of one step (warmup 0, steps 1) except the synthetic-data fill",
            "workloads": {}}

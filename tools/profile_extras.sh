@@ -3,7 +3,8 @@
 # reports under other_configs, at the sizes driver_extras() runs them: for each, two separate
 # passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass, MI355X_MICROARCH.md "PMC slots") over
 # `bench.py --workload ... --warmup 0 --steps 1 --no-cpu`, then tools/pmc_extras.py sums every
-# kernel the step launched (not the synthetic-data fill) into profiles/<tag>/extras_traffic.json.
+# kernel the step launched (not the synthetic-data fill) into profiles/extras_traffic.json (read by
+# bench.py at run time, so it lives outside the gpurun-ignored round directories).
 # usage: bash tools/profile_extras.sh <tag> [name ...]   (names: see EXTRAS below; default all)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -26,6 +27,7 @@ names=("$@")
 [ ${#names[@]} -eq 0 ] && names=(configs0 configs2 configs4 files upload process rs fullprocessing process_upload)
 for n in "${names[@]}"; do
   a="${EXTRAS[$n]} --warmup 0 --steps 1 --no-cpu"
+  mkdir -p "$out/$n"
   for c in FETCH_SIZE WRITE_SIZE; do
     echo "=== $n $c: bench.py $a"
     timeout -s KILL 300 rocprofv3 --pmc $c -d "$out/$n/$c" -o pmc --output-format csv -- python3 bench.py $a \
@@ -36,4 +38,4 @@ for n in "${names[@]}"; do
   done
   echo "$a" > "$out/$n/args.txt"
 done
-python3 tools/pmc_extras.py "$out" "profiles/$tag/extras_traffic.json"
+python3 tools/pmc_extras.py "$out" profiles/extras_traffic.json "$tag"
