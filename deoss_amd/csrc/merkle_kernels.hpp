@@ -264,15 +264,6 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t y = __shfl_xor(x, o, 64);
-        x = y < x ? y : x;
-    }
-    return x;
-}
-
 // K1: leaf SHA-256, one lane per leaf; optionally fused with the first tree levels.
 template <bool TABLE, bool ALIGNED>
 __global__ __launch_bounds__(kBlock) void leaf_kernel(LeafArgs a) {
@@ -896,27 +887,53 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
         for (int k = 0; k < 4; k++) x[k] = role_a ? st0[(k + 2) & 3] : st0[4 + k];
         const uint4* col = &ring[0][0][0][cq];   // the a-triple reads it too (and ignores it)
         __syncthreads();
-        // blocks every leaf of this wave has (inactive leaves do not count)
-        const uint64_t nb_all = wave_min_u64(vq.active ? vq.nb : ~0ull);
-        for (uint64_t it = 0; it < NI; it++) {
-            const uint4* kw = col + (it % kLatRing) * 16 * G;
-            if ((it + 1) * kQuadBlocks <= nb_all) {
-                quad_stage_regs<G, ROW, COMPACT>(x, kw + p * G, sh, msk);   // quad lane p's groups
-            } else {
-                for (uint32_t k = 0; k < kQuadBlocks; k++) {
-                    const uint4* kb = kw + k * ROW;
-                    if (it * kQuadBlocks + k < vq.nb)
-                        quad_block_skewed(x, [kb](int g) { return kb[g * G]; }, sh, msk);
+        // xf: the leaf's state after its last block.  A stage takes the register path (all 8 blocks,
+        // no per-block branch) unless some leaf of the wave ENDS strictly inside it; leaves that
+        // ended in an earlier stage run it too, on stale ring words, and keep their result in xf.
+        // (Before: the register path only while every leaf still had all 8 blocks, so a wave mixing
+        // lengths -- a FullProcessing segment beside its 4x shorter fragments, a short last chunk --
+        // ran its longest chain on the per-block path once the shortest leaf ended: 1 MiB upload
+        // 490 -> 613-719 ms of leaf kernel.)
+        uint32_t xf[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) xf[k] = x[k];
+        // a leaf of the wave ends strictly inside stage it
+        auto partial = [&](uint64_t it) {
+            const uint64_t b0 = it * kQuadBlocks;
+            return __any(vq.active && vq.nb > b0 && vq.nb < b0 + kQuadBlocks);
+        };
+        for (uint64_t it = 0; it < NI;) {
+            // runs of whole stages: their own loop, so the register path compiles (and is counted
+            // by deoss_amd/isa.py) without the per-block path inside it
+            for (; it < NI && !partial(it); it++) {
+                quad_stage_regs<G, ROW, COMPACT>(x, col + (it % kLatRing) * 16 * G + p * G, sh, msk);
+                if (vq.nb > it * kQuadBlocks) {   // this stage advanced the leaf
+#pragma unroll
+                    for (int k = 0; k < 4; k++) xf[k] = x[k];
                 }
+                __syncthreads();
+            }
+            if (it == NI) break;
+            const uint4* kw = col + (it % kLatRing) * 16 * G;
+            const uint64_t b0 = it * kQuadBlocks;
+            for (uint32_t k = 0; k < kQuadBlocks; k++) {
+                const uint4* kb = kw + k * ROW;
+                if (b0 + k < vq.nb)
+                    quad_block_skewed(x, [kb](int g) { return kb[g * G]; }, sh, msk);
+            }
+            if (vq.nb > b0) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) xf[k] = x[k];
             }
             __syncthreads();
+            it++;
         }
         // full state on the e-quad's first lane: (a,b,c,d) from the a-quad 8 lanes up
         uint32_t st[8];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            st[k] = __shfl(x[(k + 2) & 3], (int)(lane + 8), 64);
-            st[4 + k] = x[k];
+            st[k] = __shfl(xf[(k + 2) & 3], (int)(lane + 8), 64);
+            st[4 + k] = xf[k];
         }
         if (vq.active && !role_a && p == 0) {
             leaf_epilogue<ALIGNED>(a, iq, vq, st);

@@ -6,7 +6,7 @@
 // DEOSS_GPUS (default: all visible GPUs).  Each call runs whole on the least-loaded GPU, so
 // concurrent handlers spread over the node (8 concurrent NewHashTree calls over 256 x 32 MiB
 // segment files: one GPU each, ~0.5 s together), on one of the GPU's DEOSS_LANES call lanes
-// (default 2: two large calls share a GPU side by side); a call is sharded by aligned chunk ranges with
+// (4 on an MI355X: four large calls share a GPU side by side); a call is sharded by aligned chunk ranges with
 // one RCCL all-gather of subtree roots only when the library's cost model says it finishes sooner
 // and no other call is in flight (e.g. a 1 TiB object, or 1 MiB chunks bound by one PCIe link;
 // DESIGN.md §7).  Build: CGO_ENABLED=1, -tags hip, PKG_CONFIG_PATH=<checkout>/deoss_amd.

@@ -111,7 +111,7 @@ func gpu() error {
 				return
 			}
 			// one token per call lane: a coder's calls run on its context's lanes (own staging each),
-			// so that many large uploads share the GPU side by side (DEOSS_LANES, default 2)
+			// so that many large uploads share the GPU side by side (DEOSS_LANES; 4 per MI355X by default)
 			for l := 0; l < int(C.dm_lane_count(pc)); l++ {
 				pipes <- rs
 			}

@@ -206,6 +206,36 @@ def test_batch_ragged_objects(ctx, oracle_lib, leaf_mode):
     assert [got[32 * i:32 * i + 32] for i in range(len(objs))] == wants
 
 
+def test_quad_mixed_lengths_stage_boundaries(ctx, oracle_lib):
+    """K1Q over leaves of very different lengths in one wave (a FullProcessing segment beside its
+    4x shorter fragments, an object's short last chunk): whole 8-block stages stay on the register
+    path after the shorter leaves have ended (their state kept from their last block); a stage in
+    which a leaf ends takes the per-block path.  Leaves end before, at and inside stage boundaries."""
+    S = 8 * 64   # one stage of blocks
+    lens = [S * 40, S * 10, S * 10 + 64 * 3, S * 25 + 64, 64, 0, S * 3 - 1, S * 40 - 55,
+            S * 17, 1, S * 40, S * 12 + 448, S * 12 + 447, S * 2, 55, S * 31 + 9,
+            S * 40 + 200, S * 8, S * 8 + 1, S * 8 - 1]
+    chunks = [oracle_lib.splitmix_bytes(n, 4200 + i) for i, n in enumerate(lens)]
+    want_leaves, want = oracle_lib.root_chunks(chunks, nthreads=8)
+    ctx.set_leaf_kernel("quad")
+    try:
+        leaves, root = ctx.root_chunks(chunks)
+        assert leaves == want_leaves and root == want
+        # the same leaves as one-leaf objects in device memory (table mode, one launch)
+        torch = _torch()
+        keep = [dev_bytes(c) for c in chunks if c]
+        ls = [len(c) for c in chunks if c]
+        out = torch.zeros(32 * len(ls), dtype=torch.uint8, device="cuda")
+        ctx.root_batch_device_async([p for _, p in keep], ls, 1 << 30, out.data_ptr(),
+                                    torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        got = bytes(out.cpu().numpy())
+        wl = [want_leaves[32 * i:32 * i + 32] for i, c in enumerate(chunks) if c]
+        assert [got[32 * i:32 * i + 32] for i in range(len(ls))] == [hashlib.sha256(h + h).digest() for h in wl]
+    finally:
+        ctx.set_leaf_kernel("auto")
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_batch_pipelined_host(ctx, oracle_lib, pinned):
     """dm_root_batch over > 256 MiB of host objects: groups copied while earlier groups hash
@@ -588,7 +618,7 @@ def test_lanes_concurrent_calls(oracle_lib, tmp_path, monkeypatch, keep):
         c.close()
     s = _forced_sharded_context()
     try:
-        assert s.lane_count == 2   # dm_create's default
+        assert s.lane_count == 4   # dm_create's default on an MI355X (sized from free HBM)
         host = oracle_lib.splitmix_bytes(1000 * 4096 + 7, 31)
         lw, want = oracle_lib.root_buffer(host, 4096, nthreads=8)
         assert s.root_buffer(host, 4096, want_leaves=True) == (lw, want)
