@@ -34,6 +34,7 @@
 
 #include "deoss_merkle.h"
 #include "merkle_kernels.hpp"
+#include "copy_pool.hpp"
 #include "shard_plan.hpp"
 
 namespace {
@@ -203,103 +204,7 @@ struct Reaper {
 void reaper_put(Reaper* r, int dev, void* p, bool pinned) { r->put(dev, p, pinned); }
 void reaper_drain(Reaper* r) { r->drain(); }
 
-// Host copies into the pinned staging ring, spread over a few threads.  One thread's memcpy from
-// pageable memory into pinned memory runs well below PCIe (the ring's H2D side), so a pageable
-// source was copy-bound (1 MiB requests through the batcher: ~13 GiB/s).  One process-wide pool
-// (DEOSS_COPY_THREADS helpers, default 7; 0 = the caller alone) serves every lane: a call splits
-// its copies into pieces of at most kCopyPiece and copies them together with the helpers, pulling
-// pieces from a shared index, so concurrent calls share the helpers and the caller always makes
-// progress itself.
-constexpr size_t kCopyPiece = 4ull << 20;
-struct CopyItem {
-    void* dst;
-    const void* src;
-    size_t n;
-};
-class CopyPool {
-  public:
-    static CopyPool& get() {
-        static CopyPool pool;
-        return pool;
-    }
-    void run(const std::vector<CopyItem>& items) {
-        size_t total = 0;
-        for (const CopyItem& it : items) total += it.n;
-        if (total == 0) return;
-        auto job = std::make_shared<Job>();
-        for (const CopyItem& it : items)
-            for (size_t o = 0; o < it.n; o += kCopyPiece)
-                job->pieces.push_back({static_cast<uint8_t*>(it.dst) + o, static_cast<const uint8_t*>(it.src) + o,
-                                       std::min(kCopyPiece, it.n - o)});
-        const size_t helpers = std::min(nthreads_, job->pieces.size() - 1);
-        if (helpers) {
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                for (size_t h = 0; h < helpers; h++) q_.push_back(job);
-            }
-            if (helpers == 1) cv_.notify_one();
-            else cv_.notify_all();
-        }
-        work(*job);
-        std::unique_lock<std::mutex> lk(job->mu);
-        job->cv.wait(lk, [&] { return job->done == job->pieces.size(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-
-  private:
-    struct Job {
-        std::vector<CopyItem> pieces;
-        std::atomic<size_t> next{0};
-        size_t done = 0;   // guarded by mu
-        std::mutex mu;
-        std::condition_variable cv;
-    };
-    static void work(Job& j) {
-        size_t mine = 0;
-        for (size_t i; (i = j.next.fetch_add(1)) < j.pieces.size(); mine++) {
-            const CopyItem& p = j.pieces[i];
-            std::memcpy(p.dst, p.src, p.n);
-        }
-        if (mine) {
-            std::lock_guard<std::mutex> lk(j.mu);
-            j.done += mine;
-            if (j.done == j.pieces.size()) j.cv.notify_all();
-        }
-    }
-    CopyPool() {
-        const char* v = std::getenv("DEOSS_COPY_THREADS");
-        nthreads_ = v && *v ? (size_t)std::max(0, std::atoi(v)) : 7;
-        for (size_t t = 0; t < nthreads_; t++)
-            th_.emplace_back([this] {
-                for (;;) {
-                    std::shared_ptr<Job> j;
-                    {
-                        std::unique_lock<std::mutex> lk(mu_);
-                        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                        if (q_.empty()) return;
-                        j = q_.front();
-                        q_.pop_front();
-                    }
-                    work(*j);
-                }
-            });
-    }
-    size_t nthreads_ = 0;
-    std::mutex mu_;
-    std::condition_variable cv_;
-    std::deque<std::shared_ptr<Job>> q_;
-    std::vector<std::thread> th_;
-    bool stop_ = false;
-};
-
-void par_copy(const std::vector<CopyItem>& items) { CopyPool::get().run(items); }
+void par_copy(const std::vector<dm_copy::CopyItem>& items) { dm_copy::CopyPool::get().run(items); }
 
 // The HIP resources of one streaming upload (dm_stream / dm_pstream), pooled per device and reused
 // by the next stream: creating streams and pinning staging costs ~10 ms per object
@@ -1018,7 +923,7 @@ int h2d_at(dm_ctx* c, Dev& d, const void* const* ptrs, const uint64_t* lens, uin
     int slot = 0;
     bool busy[2] = {false, false};
     uint64_t fill = 0, slot_dev_off = 0;
-    std::vector<CopyItem> pending;   // this slot's host copies, done together at flush (par_copy)
+    std::vector<dm_copy::CopyItem> pending;   // this slot's host copies, done together at flush (par_copy)
     auto flush = [&]() -> int {
         if (fill == 0) return DM_OK;
         par_copy(pending);   // while the other slot's H2D is in flight
@@ -1169,7 +1074,7 @@ int h2d_and_hash_leaves(dm_ctx* c, Dev& d, const void* host, uint64_t len, uint6
         } else {
             if (busy[slot]) HIP_TRY(hipEventSynchronize(d.ev_copy[slot]));
             uint8_t* st = d.stage[slot].u8();
-            std::vector<CopyItem> rows;
+            std::vector<dm_copy::CopyItem> rows;
             rows.reserve(n);
             for (uint64_t r = 0; r + 1 < n; r++) rows.push_back({st + r * w, src + r * chunk + b0, (size_t)w});
             if (last_w) rows.push_back({st + (n - 1) * w, src + (n - 1) * chunk + b0, (size_t)last_w});

@@ -38,7 +38,7 @@ def test_lane_growth_near_full_hbm_waits_for_deferred_frees(oracle_lib):
     import numpy as np
     torch = _torch()
     from deoss_amd import MerkleContext
-    small, big = 2 << 30, 3 << 30
+    small, big = 4 << 30, 6 << 30
     host = np.empty(big, dtype=np.uint8)                 # pageable: the copy path grows d.data
     oracle_lib.fill_splitmix_ptr(host.ctypes.data, 0, big, 0xDE0554400)
     _, want_small = oracle_lib.root_buffer_ptr(host.ctypes.data, small, CHUNK, nthreads=16)
@@ -50,15 +50,17 @@ def test_lane_growth_near_full_hbm_waits_for_deferred_frees(oracle_lib):
     root_b = torch.zeros(32, dtype=torch.uint8, device="cuda")
     hog = None
     try:
-        assert a.root_buffer_ptr(host.ctypes.data, small, CHUNK)[1] == want_small   # a's lane holds ~2 GiB
+        assert a.root_buffer_ptr(host.ctypes.data, small, CHUNK)[1] == want_small   # a's lane holds ~4 GiB
         torch.cuda.synchronize()
         free, _ = torch.cuda.mem_get_info()
-        hog = torch.empty(free - (2 << 30), dtype=torch.uint8, device="cuda")   # ~2 GiB left < 3 GiB
+        # ~5 GiB left: below the 6 GiB growth, but with the 4 GiB old block freed there is room
+        # for it plus 3 GiB for everything else the call and the HIP runtime allocate
+        hog = torch.empty(free - (5 << 30), dtype=torch.uint8, device="cuda")
         free_left, _ = torch.cuda.mem_get_info()
-        assert free_left < big
+        assert free_left < big < free_left + small
         side = torch.cuda.Stream()
         b.root_device_async(dev.data_ptr(), 1 << 30, CHUNK, root_b.data_ptr(), 0, side.cuda_stream)
-        got = a.root_buffer_ptr(host.ctypes.data, big, CHUNK)[1]         # grows 2 -> 3 GiB meanwhile
+        got = a.root_buffer_ptr(host.ctypes.data, big, CHUNK)[1]         # grows 4 -> 6 GiB meanwhile
         torch.cuda.synchronize()
         assert got == want_big
     finally:
