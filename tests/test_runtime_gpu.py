@@ -38,6 +38,11 @@ def test_lane_growth_near_full_hbm_waits_for_deferred_frees(oracle_lib):
     import numpy as np
     torch = _torch()
     from deoss_amd import MerkleContext
+    trace = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "libsegv_trace.so")
+    arm = None
+    if os.path.exists(trace):   # diagnostic: native backtrace if this test ever faults on the host
+        import ctypes
+        arm = ctypes.CDLL(trace).segv_trace_install
     small, big = 4 << 30, 6 << 30
     host = np.empty(big, dtype=np.uint8)                 # pageable: the copy path grows d.data
     oracle_lib.fill_splitmix_ptr(host.ctypes.data, 0, big, 0xDE0554400)
@@ -60,6 +65,8 @@ def test_lane_growth_near_full_hbm_waits_for_deferred_frees(oracle_lib):
         assert free_left < big < free_left + small
         side = torch.cuda.Stream()
         b.root_device_async(dev.data_ptr(), 1 << 30, CHUNK, root_b.data_ptr(), 0, side.cuda_stream)
+        if arm is not None:
+            arm()
         got = a.root_buffer_ptr(host.ctypes.data, big, CHUNK)[1]         # grows 4 -> 6 GiB meanwhile
         torch.cuda.synchronize()
         assert got == want_big
