@@ -58,6 +58,9 @@ struct Reaper;
 void reaper_put(Reaper* r, int dev, void* p, bool pinned);
 void reaper_drain(Reaper* r);
 
+// Device memory a DevBuf growth leaves free for the HIP runtime and everything else (DevBuf::ensure).
+constexpr size_t kMallocHeadroom = 256ull << 20;
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -77,6 +80,21 @@ struct DevBuf {
             cap = 0;
         }
         size_t c = round_up(std::max<size_t>(n, 4096), 2ull << 20);
+        if (rp) {
+            // Near full HBM, first let the frees already queued in the reaper happen, and do not ask
+            // hipMalloc for more than is free: measured on MI355X (ROCm 7), a hipMalloc that runs
+            // out of memory while the reaper's hipFree of a large block is still pending crashed
+            // inside the HSA runtime (pthread_mutex_lock; tests/test_runtime_gpu.py, round 4).
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr < c + kMallocHeadroom) {
+                reaper_drain(rp);
+                if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr < c + kMallocHeadroom) {
+                    (void)hipGetLastError();
+                    return hipErrorOutOfMemory;
+                }
+            }
+            (void)hipGetLastError();
+        }
         hipError_t e = hipMalloc(&p, c);
         if (e == hipErrorOutOfMemory && rp) {
             // the memory this growth needs may still sit in the reaper's queue (this buffer's old

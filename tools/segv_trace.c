@@ -43,8 +43,11 @@ void segv_trace_install(void) {
     sa.sa_sigaction = on_fault;
     sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
     sigemptyset(&sa.sa_mask);
-    sigaction(SIGSEGV, &sa, &prev_segv);
-    sigaction(SIGBUS, &sa, &prev_bus);
+    struct sigaction old;
+    sigaction(SIGSEGV, &sa, &old);
+    if (!((old.sa_flags & SA_SIGINFO) && old.sa_sigaction == on_fault)) prev_segv = old;   /* never chain to itself */
+    sigaction(SIGBUS, &sa, &old);
+    if (!((old.sa_flags & SA_SIGINFO) && old.sa_sigaction == on_fault)) prev_bus = old;
 }
 
 __attribute__((constructor)) static void install(void) { segv_trace_install(); }
