@@ -825,7 +825,8 @@ def latency_block(args, torch, dev_index):
     for pinned in (False, True):
         name = "crossover_NewHashTreeFromBuffer_1MiB" + ("_pinned" if pinned else "")
         try:
-            out[name] = crossover(B_ROOT, 1 << 20, (1, 64, 512, 2048), chunk, pinned)
+            # at most 512 caller threads: a GPU box caps the processes / threads a job may run
+            out[name] = crossover(B_ROOT, 1 << 20, (1, 64, 256, 512), chunk, pinned)
         except Exception as e:
             out[name] = {"error": f"{type(e).__name__}: {e}"}
     out["bit_exact"] = all(v.get("bit_exact") is True for k, v in out.items() if isinstance(v, dict) and
