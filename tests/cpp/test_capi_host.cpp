@@ -229,6 +229,21 @@ int main(int argc, char** argv) {
     EXPECT(dm_set_leaf_kernel(c, DM_LEAF_AUTO) == DM_OK);
     check_buffer(c, (300ull << 20) + 3, 64ull << 20, 5);   // striped host path
 
+    // where the last call ran (round 4): one device, a valid lane; no exchange without sharding
+    {
+        int devs[4] = {-1, -1, -1, -1}, ids[4] = {-1, -1, -1, -1}, lane = -9;
+        EXPECT(dm_last_call_devices(c, devs, ids, 4, &lane) == 1);
+        EXPECT(devs[0] == 0 && ids[0] == 0 && lane >= 0 && lane < dm_lane_count(c));
+        EXPECT(dm_last_call_devices(nullptr, devs, ids, 4, &lane) == DM_ERR_INVALID);
+        uint64_t xn = 9;
+        double xs = -1, xm = -1;
+        int xg = -1;
+        EXPECT(dm_set_timing(c, 1) == DM_OK);
+        check_buffer(c, (3u << 20) + 5, 4096, 6);
+        EXPECT(dm_exchange_timing(c, &xn, &xs, &xm, &xg) == DM_OK && xn == 0 && xs == 0 && xg == 0);
+        EXPECT(dm_set_timing(c, 0) == DM_OK);
+    }
+
     // chunk list with empty chunks, and batches
     std::vector<std::vector<uint8_t>> ch;
     for (int i = 0; i < 37; i++) ch.push_back(bytes((i * 977) % 5000, 100 + i));
