@@ -31,6 +31,28 @@ ISSUE_CYCLES_ONE_WAVE = 4             # one wave alone issues a VALU instruction
 SEED = 0xDE0550002               # configs[1] seed (0xDE0550000 + k)
 
 
+PHASE = ["start"]   # what the run is doing now (stderr progress lines, heartbeat)
+
+
+def progress(phase: str) -> None:
+    """One stderr line per phase (stdout carries only the JSON line), and the heartbeat's label."""
+    PHASE[0] = phase
+    print(f"[bench] {time.strftime('%H:%M:%S')} {phase}", file=sys.stderr, flush=True)
+
+
+def start_heartbeat(period_s: float = 50.0) -> None:
+    """A daemon thread that prints the current phase to stderr every period_s: a long default run
+    (N = 1: headline, extras, latency) never goes silent for minutes."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period_s)
+            print(f"[bench] {time.strftime('%H:%M:%S')} ... {PHASE[0]}", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def env_int(name, default):
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
@@ -218,6 +240,8 @@ def main() -> None:
         launch_check(args)
         return
 
+    start_heartbeat()
+    progress(f"bench.py {' '.join(sys.argv[1:])}")
     import torch
     import torch.distributed as dist
     from deoss_amd import MerkleContext, plan_shards
@@ -273,6 +297,7 @@ def main() -> None:
                 dist.barrier(device_ids=[dev_index])
         torch.cuda.synchronize()
 
+    progress("headline: timed steps")
     out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
     if isinstance(out.get("parity"), dict):
         out["parity"]["pinned_by"] = PIN_MERKLE
@@ -280,9 +305,11 @@ def main() -> None:
         out["launch"] = launch_info(torch, dist, world, rank, local_rank, dev_index, args)
     if world == 1 and rank == 0 and not args.no_extras:
         out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
+        progress("latency block")
         out["latency"] = latency_block(args, torch, dev_index)
     if ((world == 8 and not args.same_device) or (world > 1 and args.multi_configs)) and not args.no_extras \
             and not args.total_gib:
+        progress("multi-GPU configs (configs[3], configs[4])")
         other = multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         if rank == 0:
             out["other_configs"] = other
@@ -291,6 +318,7 @@ def main() -> None:
         torch.cuda.empty_cache()
         dist.barrier(group=wait_group)
         inproc, hung = None, False
+        progress("in-process leg (rank 0 over every GPU)")
         if rank == 0:
             inproc, hung = run_with_watchdog(lambda: in_process_configs(args, torch, world), args.inproc_timeout)
         flag = torch.tensor([1 if hung else 0], dtype=torch.int64)
@@ -1153,6 +1181,7 @@ def driver_extras(args, torch, dist, device, dev_index):
     res = {}
     traffic, tsrc = extras_traffic()
     for name, fn, kw in specs:
+        progress(f"extra {name}")
         ns = copy.copy(args)
         ns.__dict__.update(kw)
         t0 = time.perf_counter()
@@ -2385,6 +2414,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         host.copy_(buf[:length])
         torch.cuda.synchronize()
     if not args.no_cpu:
+        progress("CPU baseline over the headline object")
         # faithful serial restatement of common/hashtree over the same 8 GiB (1 core, SHA-NI when present)
         facts = host_cpu_facts()
         t0 = time.perf_counter()
@@ -2426,6 +2456,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         out["parity"] = {"gpu_root": root_hex, "cpu_root": cpu_root.hex(),
                          "bit_exact": cpu_root.hex() == root_hex and cpu_root_p == cpu_root}
     if do_e2e and host is not None:
+        progress("host-buffer end to end")
         # host pinned buffer -> H2D (overlapped) -> root -> 32 B back (the upload-handler path)
         ctx.root_buffer_ptr(host.data_ptr(), min(length, 64 << 20), chunk)   # warm staging
         t0 = time.perf_counter()
@@ -2450,6 +2481,7 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         # the GPU / host crossover: 1 MiB and 64 KiB chunks of the same object
         args.sweep, args.sweep_chunks = True, "65536,1048576"
     if args.sweep and not args.no_sweep:
+        progress("chunk-size sweep")
         sweep = []
         root = torch.zeros(32, dtype=torch.uint8, device=buf.device)
         modes = ["wide", "latency", "pair", "quad"] if args.sweep_modes else ["auto"]

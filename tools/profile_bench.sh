@@ -7,7 +7,7 @@ set -e
 out=$1
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py > $out/bench_kt.json
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py > $out/bench_kt.json
 P="--no-extras --no-e2e --no-sweep --no-cpu --steps 2 --warmup 1"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o fetch --output-format csv -- python3 bench.py $P > $out/bench_fetch.json
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $out/write -o write --output-format csv -- python3 bench.py $P > $out/bench_write.json
