@@ -1102,19 +1102,34 @@ def measure_read_peak(ctx, torch, buf, nbytes, sptr, stream, reps=5):
 
 PCIE_PEAK_GBS = 64.0   # PCIe 5.0 x16, one direction, raw (about 55 GB/s measured)
 # Step-level roofline of each N = 1 extra: (profiles/extras_traffic.json key, bound, algorithmic
-# bytes one step must move on the bound's link, what they are).  Sizes are driver_extras()'s.
+# bytes one step must move on the bound's link, what they are, the bytes this design's own kernels
+# must move on the memory side per step, what those are).  Sizes are driver_extras()'s.  The PMC
+# traffic of the kernels is compared with the design bytes; the blit copies (__amd_rocclr_*) are
+# reported apart, since their counter widths across PCIe are uncalibrated.
 EXTRA_ROOF = {
-    "configs[0]": ("configs0", "hbm", (64 << 20) + 2 * 32, "read the 64 MiB object once + 2 leaf digests"),
-    "configs[2]": ("configs2", "hbm", 4096 * (4 << 20) + 4096 * 32, "read 4,096 x 4 MiB once + one digest each"),
+    "configs[0]": ("configs0", "hbm", (64 << 20) + 2 * 32, "read the 64 MiB object once + 2 leaf digests",
+                   64 << 20, "the leaf kernel reads the object once"),
+    "configs[2]": ("configs2", "hbm", 4096 * (4 << 20) + 4096 * 32, "read 4,096 x 4 MiB once + one digest each",
+                   4096 * (4 << 20), "the leaf kernel reads every object once"),
     "configs[4]_per_gpu_share": ("configs4", "pcie", 12500 * (1 << 20) + 12500 * 32,
-                                 "12,500 x 1 MiB read once from pinned host memory (zero-copy K1Q over PCIe)"),
-    "files_NewHashTree": ("files", "pcie", 256 * (32 << 20), "256 x 32 MiB files: every byte H2D once"),
-    "upload_stream_1MiB_chunks": ("upload", "pcie", 8 << 30, "8 GiB pageable body: every byte H2D once"),
-    "FullProcessing": ("process", "hbm", (8 << 30) * 6,
-                       "RS reads 8 GiB, writes 16 GiB of parity; the leaf kernel re-reads all 24 GiB (unfused)"),
-    "reed_solomon_4+8": ("rs", "hbm", (8 << 30) * 3, "read 8 GiB of segments, write 16 GiB of parity"),
-    "FullProcessing_file": ("fullprocessing", "pcie", (2 << 30) * 3, "2 GiB file H2D + 4 GiB parity D2H"),
-    "FullProcessing_while_receiving": ("process_upload", "pcie", (2 << 30) * 3, "2 GiB body H2D + 4 GiB parity D2H"),
+                                 "12,500 x 1 MiB read once from pinned host memory (zero-copy K1Q over PCIe)",
+                                 12500 * (1 << 20), "the leaf kernel reads every object once from pinned memory"),
+    "files_NewHashTree": ("files", "pcie", 256 * (32 << 20), "256 x 32 MiB files: every byte H2D once",
+                          256 * (32 << 20), "the leaf kernel reads the pinned staging once (zero-copy)"),
+    "upload_stream_1MiB_chunks": ("upload", "pcie", 8 << 30, "8 GiB pageable body: every byte H2D once",
+                                  8 << 30, "the leaf kernel reads the pinned staging once (zero-copy)"),
+    "FullProcessing": ("process", "hbm", (8 << 30) * 7,
+                       "RS reads 8 GiB and writes 16 GiB of parity; the leaf kernel reads the 8 GiB of segments "
+                       "and all 24 GiB of fragments (the data fragments are the segments' bytes again: unfused; "
+                       "a single-read fused pipeline would move 24 GiB)",
+                       (8 << 30) * 7, "RS 8 GiB read + 16 GiB written, leaf 32 GiB read"),
+    "reed_solomon_4+8": ("rs", "hbm", (8 << 30) * 3, "read 8 GiB of segments, write 16 GiB of parity",
+                         (8 << 30) * 3, "RS 8 GiB read + 16 GiB written"),
+    "FullProcessing_file": ("fullprocessing", "pcie", (2 << 30) * 3, "2 GiB file H2D + 4 GiB parity D2H",
+                            (2 << 30) * 7, "RS 2 GiB read + 4 GiB written, leaf 8 GiB read (segments + fragments)"),
+    "FullProcessing_while_receiving": ("process_upload", "pcie", (2 << 30) * 3, "2 GiB body H2D + 4 GiB parity D2H",
+                                       (2 << 30) * 7,
+                                       "RS 2 GiB read + 4 GiB written, leaf 8 GiB read (segments + fragments)"),
 }
 
 
@@ -1133,19 +1148,26 @@ def extra_roofline(name, r, traffic, src):
     A kernel-level roofline the workload reports itself is kept under "kernel_level"."""
     if name not in EXTRA_ROOF or not isinstance(r, dict) or not r.get("ms_per_step"):
         return
-    key, bound, alg, what = EXTRA_ROOF[name]
+    key, bound, alg, what, design, design_what = EXTRA_ROOF[name]
     e = traffic.get(key) or {}
     peak = HBM_PEAK_GBS if bound == "hbm" else PCIE_PEAK_GBS
     ach = alg / (r["ms_per_step"] * 1e-3) / 1e9
     roof = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": "GB/s", "frac": round(ach / peak, 6),
             "traffic": e.get("traffic_bytes_per_step"), "algorithmic_bytes_per_step": alg, "what": what,
             "time_basis": "ms_per_step (the whole step, wall clock)",
-            "traffic_scope": (f"{src}[{key}]: memory-side bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE) of every kernel one "
-                              "step launches; host-memory reads by the zero-copy kernels count too") if e else
+            "traffic_scope": (f"{src}[{key}]: memory-side bytes (PMC FETCH_SIZE x 2 + WRITE_SIZE) of every kernel "
+                              "and blit copy of one warm step (PMC of 2 steps - PMC of 1 step); host-memory "
+                              "reads by the zero-copy kernels count too") if e else
                              "not profiled"}
     if e:
         roof["traffic_over_algorithmic"] = round(e["traffic_bytes_per_step"] / alg, 4)
         roof["traffic_kernels"] = {k: round(v["read_bytes"] + v["write_bytes"]) for k, v in e["kernels"].items()}
+        kern = sum(v["read_bytes"] + v["write_bytes"] for k, v in e["kernels"].items() if not k.startswith("__amd_"))
+        roof.update({"design_kernel_bytes_per_step": design, "design_what": design_what,
+                     "kernel_traffic": round(kern), "kernel_traffic_over_design": round(kern / design, 4),
+                     "copy_traffic": round(e["traffic_bytes_per_step"] - kern)})
+        if e.get("method"):
+            roof["traffic_method"] = e["method"]
     if isinstance(r.get("roofline"), dict):
         kl = dict(r["roofline"])
         if kl.get("traffic") is None and e:   # the kernel-level line's own kernel, from the same passes

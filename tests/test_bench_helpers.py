@@ -23,14 +23,18 @@ def test_percentiles_nearest_rank():
 def test_extra_roofline_step_level_and_kernel_level():
     traffic = {"process": {"traffic_bytes_per_step": 52e9, "kernels": {
         "rs_code_kernel": {"launches": 1, "read_bytes": 8.6e9, "write_bytes": 17.2e9},
-        "leaf_kernel_quad": {"launches": 1, "read_bytes": 25.9e9, "write_bytes": 1e5}}}}
+        "leaf_kernel_quad": {"launches": 1, "read_bytes": 25.9e9, "write_bytes": 1e5},
+        "__amd_rocclr_copyBuffer": {"launches": 2, "read_bytes": 0.1e9, "write_bytes": 0.2e9}}}}
     r = {"ms_per_step": 600.0, "roofline": {"bound": "hbm", "achieved": 52.0, "frac": 0.0065, "traffic": None}}
     bench.extra_roofline("FullProcessing", r, traffic, "profiles/extras_traffic.json")
     rf = r["roofline"]
-    alg = (8 << 30) * 6
+    alg = (8 << 30) * 7
     assert rf["bound"] == "hbm" and rf["algorithmic_bytes_per_step"] == alg
     assert abs(rf["achieved"] - alg / 0.6 / 1e9) < 1e-3 and rf["frac"] == round(rf["achieved"] / 8000.0, 6)
     assert rf["traffic"] == 52e9 and abs(rf["traffic_over_algorithmic"] - 52e9 / alg) < 1e-4
+    kern = 8.6e9 + 17.2e9 + 25.9e9 + 1e5           # the product's kernels; the blit copies apart
+    assert rf["kernel_traffic"] == round(kern) and rf["copy_traffic"] == round(52e9 - kern)
+    assert rf["kernel_traffic_over_design"] == round(kern / rf["design_kernel_bytes_per_step"], 4)
     kl = rf["kernel_level"]             # the workload's own kernel-level line, traffic filled in
     assert kl["traffic"] == 25.9e9 + 1e5 and "leaf_kernel_quad" in kl["traffic_source"]
     # host-memory extras are bound by the PCIe link; an unprofiled extra says so

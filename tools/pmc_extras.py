@@ -1,6 +1,6 @@
 """Per-step memory-side traffic of the extra workloads from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-Usage: python tools/pmc_extras.py <gpurun_out/<tag>_pmc> <out.json> [tag]
+Usage: python tools/pmc_extras.py <gpurun_out/<tag>_pmc | profiles/r04/extras_pmc> <out.json> [tag]
 
 Input (tools/profile_extras.sh): <dir>/<name>/s<K>/{FETCH_SIZE,WRITE_SIZE}/**/*counter_collection.csv,
 one `bench.py --workload ... --warmup 0 --steps K` run per pass, K = 1 and 2.  One step's traffic
@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import csv
 import glob
+import gzip
 import json
 import os
 import sys
@@ -33,8 +34,8 @@ def short(name: str) -> str:
 
 def dispatches(path_glob):
     rows = []
-    for path in sorted(glob.glob(path_glob, recursive=True)):
-        with open(path) as f:
+    for path in sorted(glob.glob(path_glob, recursive=True) + glob.glob(path_glob + ".gz", recursive=True)):
+        with (gzip.open(path, "rt") if path.endswith(".gz") else open(path)) as f:
             for r in csv.DictReader(f):
                 rows.append((int(r.get("Dispatch_Id", 0) or 0), r["Kernel_Name"], int(r["Grid_Size"]),
                              float(r["Counter_Value"])))
@@ -46,6 +47,9 @@ def per_kernel(d, skip):
     """{kernel: [launches, read_bytes, write_bytes]} of one run's two passes, or None."""
     fr = dispatches(os.path.join(d, "FETCH_SIZE", "**", "*counter_collection.csv"))
     wr = dispatches(os.path.join(d, "WRITE_SIZE", "**", "*counter_collection.csv"))
+    if not fr and not wr:      # the archived layout: <d>/{FETCH_SIZE,WRITE_SIZE}_counter_collection.csv.gz
+        fr = dispatches(os.path.join(d, "FETCH_SIZE_counter_collection.csv"))
+        wr = dispatches(os.path.join(d, "WRITE_SIZE_counter_collection.csv"))
     if not fr or not wr:
         return None
     out = {}
