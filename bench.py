@@ -720,13 +720,33 @@ def latency_block(args, torch, dev_index):
         for name, nbytes, reps in (("FullProcessing_1MiB", 1 << 20, 12), ("FullProcessing_64MiB", 64 << 20, 6)):
             try:
                 a = host(nbytes, SEED + 0x600 + nbytes)
-                src = (ctypes.c_char * nbytes).from_address(a.ctypes.data)
-                gx, g = timed(lambda: proc.process_buffer(src, want_frags=True), reps)
-                cx, c = timed(lambda: orc.full_processing_ptr(a.ctypes.data, nbytes, seg, 4, 8, want_frags=True,
-                                                              nthreads=1), reps)
-                out[name] = entry(gx, cx, g[0] == c[0] and g[1] == c[1] and g[2] == c[2] and g[3] == c[3],
-                                  what=f"{nbytes} B upload -> {-(-nbytes // seg)} zero-padded 32 MiB segment(s), "
-                                       "RS 4+8, every segment / fragment digest, fid, fragments back in host memory")
+                nseg = -(-nbytes // seg)
+                # the C calls alone, into output buffers allocated and touched once (as a handler that
+                # reuses its buffers): Python's allocation and bytes copies stay out of both legs
+                bufs = {side: [np.ones(x, dtype=np.uint8) for x in (32 * nseg, 32 * nseg * 12, 32,
+                                                                    nseg * 12 * (seg // 4))]
+                        for side in ("gpu", "cpu")}
+
+                def gpu_call(b=bufs["gpu"]):
+                    proc._check(proc.ctx._L.dm_process_buffer(
+                        proc.enc._h, ctypes.c_void_p(a.ctypes.data), nbytes, seg, ctypes.c_void_p(b[3].ctypes.data),
+                        ctypes.c_void_p(b[0].ctypes.data), ctypes.c_void_p(b[1].ctypes.data),
+                        ctypes.c_void_p(b[2].ctypes.data)), "dm_process_buffer")
+
+                def cpu_call(b=bufs["cpu"]):
+                    rc = orc.L.or_full_processing(ctypes.c_void_p(a.ctypes.data), nbytes, seg, 4, 8,
+                                                  ctypes.c_void_p(b[0].ctypes.data), ctypes.c_void_p(b[1].ctypes.data),
+                                                  ctypes.c_void_p(b[2].ctypes.data), ctypes.c_void_p(b[3].ctypes.data), 1)
+                    if rc < 0:
+                        raise ValueError(f"or_full_processing rc={rc}")
+
+                gx, _ = timed(gpu_call, reps)
+                cx, _ = timed(cpu_call, reps)
+                ok = all(np.array_equal(x, y) for x, y in zip(bufs["gpu"], bufs["cpu"]))
+                out[name] = entry(gx, cx, ok,
+                                  what=f"{nbytes} B upload -> {nseg} zero-padded 32 MiB segment(s), RS 4+8, every "
+                                       "segment / fragment digest, fid, fragments back in host memory "
+                                       "(dm_process_buffer vs or_full_processing: the C calls, outputs preallocated)")
             except Exception as e:
                 out[name] = {"error": f"{type(e).__name__}: {e}"}
         try:
@@ -827,17 +847,24 @@ def latency_block(args, torch, dev_index):
         try:
             gpu_wave(max(cs))   # warm every slot's buffers at the largest wave
             with ThreadPoolExecutor(share) as ex:
-                for c in cs:
-                    tg, good = gpu_wave(c)
-                    t = time.perf_counter()
-                    got = list(ex.map(want, range(c)))
-                    tc = time.perf_counter() - t
-                    good = good and all(got[j] == wants[j % pool_n] for j in range(c))
+                for c in cs:   # each side: the better of 2 waves (Python thread start-up is noisy)
+                    w1, w2 = gpu_wave(c), gpu_wave(c)
+                    tg, good = min(w1[0], w2[0]), w1[1] and w2[1]
+                    tcs = []
+                    for _ in range(2):
+                        t = time.perf_counter()
+                        got = list(ex.map(want, range(c)))
+                        tcs.append(time.perf_counter() - t)
+                        good = good and all(got[j] == wants[j % pool_n] for j in range(c))
+                    tc = min(tcs)
                     ok = ok and good
                     rows.append({"concurrent": c, "gpu_ms": round(tg * 1e3, 2), "cpu_ms": round(tc * 1e3, 2),
                                  "gpu_faster": tg < tc})
-                    if first is None and tg < tc:
-                        first = c
+            # the smallest c from which the GPU finishes first at every larger c measured too
+            for r in reversed(rows):
+                if not r["gpu_faster"]:
+                    break
+                first = r["concurrent"]
         finally:
             b.close()
             if pin is not None:

@@ -30,6 +30,7 @@ struct BatchReq {
     int rc = DM_OK;
     std::string err;
     bool done = false;
+    std::chrono::steady_clock::time_point arrived{};
 };
 
 thread_local std::string t_batcher_err;
@@ -48,6 +49,8 @@ struct dm_batcher {
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
     std::deque<BatchReq*> q;
+    uint64_t q_leaves = 0;   // leaves queued
+    int busy = 0;            // slots running a batch
     bool stop = false;
     uint64_t n_req = 0, n_batch = 0, max_batch = 0;
 };
@@ -115,10 +118,25 @@ void batcher_worker(dm_batcher* b, size_t slot) {
             std::unique_lock<std::mutex> lk(b->mu);
             b->cv_work.wait(lk, [&] { return b->stop || !b->q.empty(); });
             if (b->q.empty()) return;   // stop requested and nothing left to drain
-            if (b->linger_us && !b->stop) {   // let a burst accumulate before launching
-                b->cv_work.wait_for(lk, std::chrono::microseconds(b->linger_us), [&] { return b->stop; });
-                if (b->q.empty()) continue;    // another slot took them meanwhile
+            // let a burst accumulate before launching (dm_plan::batch_linger_us), re-evaluated
+            // whenever a slot frees up or the queue fills a batch
+            while (!b->stop && !b->q.empty() && b->q_leaves < b->max_leaves) {
+                double chain_us = 0;
+                if (b->busy > 0) {
+                    uint64_t longest = 0;
+                    for (const BatchReq* r : b->q)
+                        longest = std::max(longest, b->mode == DM_BATCH_PROCESS ? b->unit : std::min(r->len, b->unit));
+                    chain_us = (double)ceil_div(longest + 9, 64) * dm_plan::chain_ns_per_block(dm_plan::kQuad) * 1e-3;
+                }
+                const double w = dm_plan::batch_linger_us(b->linger_us, chain_us, b->busy, (int)b->workers.size());
+                const auto until = b->q.front()->arrived + std::chrono::microseconds((int64_t)w);
+                if (std::chrono::steady_clock::now() >= until) break;
+                const int busy0 = b->busy;
+                b->cv_work.wait_until(lk, until, [&] {
+                    return b->stop || b->q.empty() || b->q_leaves >= b->max_leaves || b->busy != busy0;
+                });
             }
+            if (b->q.empty()) continue;    // another slot took them meanwhile
             uint64_t leaves = 0, bytes = 0;
             while (!b->q.empty()) {
                 BatchReq* r = b->q.front();
@@ -127,8 +145,10 @@ void batcher_worker(dm_batcher* b, size_t slot) {
                 batch.push_back(r);
                 leaves += r->leaves;
                 bytes += rb;
+                b->q_leaves -= r->leaves;
                 b->q.pop_front();
             }
+            b->busy++;
             b->n_batch++;
             b->max_batch = std::max<uint64_t>(b->max_batch, batch.size());
             if (!b->q.empty()) b->cv_work.notify_one();   // another slot can start on the rest
@@ -138,6 +158,7 @@ void batcher_worker(dm_batcher* b, size_t slot) {
         const std::string msg = rc == DM_OK ? std::string() : c->err;
         {
             std::lock_guard<std::mutex> lk(b->mu);
+            b->busy--;
             for (BatchReq* r : batch) {
                 r->rc = rc;
                 r->err = msg;
@@ -145,6 +166,7 @@ void batcher_worker(dm_batcher* b, size_t slot) {
             }
         }
         b->cv_done.notify_all();
+        b->cv_work.notify_all();   // a lingering slot re-evaluates with one busy slot fewer
     }
 }
 
@@ -155,10 +177,12 @@ int batcher_submit(dm_batcher* b, BatchReq& r) {
             t_batcher_err = "batcher is shutting down";
             return DM_ERR_INVALID;
         }
+        r.arrived = std::chrono::steady_clock::now();
         b->q.push_back(&r);
+        b->q_leaves += r.leaves;
         b->n_req++;
     }
-    b->cv_work.notify_one();
+    b->cv_work.notify_all();   // idle slots start; a lingering one re-checks the leaf budget
     std::unique_lock<std::mutex> lk(b->mu);
     b->cv_done.wait(lk, [&] { return r.done; });
     t_batcher_err = r.err;

@@ -173,6 +173,20 @@ inline int route(uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, int G, 
     return best;
 }
 
+// Coalescing executor (dm_batcher): how long a free worker slot holds a burst open, counted from
+// the arrival of the oldest queued request.  base_us is the caller's linger.  When other slots are
+// already running batches, a burst that starts now would otherwise be cut into one small batch per
+// free slot, and whatever arrives after the last slot is taken waits a whole chain (chain_us, the
+// longest queued request's leaf chain).  So the wait grows with the share of busy slots: the last
+// free slot of 4 holds the burst open for 9/256 of a chain (17 ms of a 32 MiB segment's 490 ms),
+// an idle executor launches after base_us, and a queue whose oldest request has waited that long
+// already (a freed slot under steady load) launches at once.
+inline double batch_linger_us(double base_us, double chain_us, int busy, int slots) {
+    if (busy <= 0 || slots <= 0) return base_us;
+    const double f = (double)std::min(busy, slots) / (double)slots;
+    return base_us + chain_us * f * f / 16.0;
+}
+
 // Call lanes (dm_ctx): loads[l * nphys + p] = calls running or queued on lane l of GPU p (plus
 // open streams).  A call that can run anywhere goes to the GPU whose lanes carry the least load
 // (GPUs scanned from `start`, the first minimum wins, so ties rotate with `start`), then to that

@@ -330,8 +330,12 @@ enum { DM_BATCH_ROOT = 0, DM_BATCH_PROCESS = 1 };
  * requests spread over the GPUs with no exchange.  mode ROOT: unit = chunk size (each request:
  * NewHashTreeFromBuffer); PROCESS: unit = segment size with data/parity shards (each request:
  * FullProcessing).  slots (0 = 4) worker contexts per GPU; max_leaves / max_bytes per batch
- * (0 = 4096 leaves / 16 GiB); linger_us: how long a worker waits for more requests after the
- * first before launching (0 = at once). */
+ * (0 = 4096 leaves / 16 GiB); linger_us: how long a free worker holds a burst open for more
+ * requests, counted from the oldest queued request's arrival (0 = at once).  While other slots
+ * are running batches the wait grows with their share (the last free slot of 4 waits 9/256 of
+ * the longest queued request's chain more: 17 ms for a 32 MiB segment), so a burst that starts
+ * during a running batch is not cut into one small batch per free slot; a full batch's worth of
+ * leaves queued, or an oldest request that has already waited that long, launches at once. */
 int dm_batcher_create(const int *devs, int ndev, int mode, uint64_t unit, int data_shards, int parity_shards,
                       int slots, uint64_t max_leaves, uint64_t max_bytes, uint32_t linger_us, dm_batcher **out);
 /* Drains queued requests, then frees the workers and their contexts. */

@@ -155,6 +155,21 @@ int main(int argc, char** argv) {
         CHECK(spread, "16 calls over 16 lanes");
         CHECK(dm_plan::pick_lane(loads, 8, 2, 3, 6) == 6, "fixed GPU: its lane 0 on ties");
     }
+    {   // batcher linger: the caller's base while no slot is busy, growing with the busy share
+        const double chain = 490e3;                           // one 32 MiB segment chain, us
+        CHECK(dm_plan::batch_linger_us(2000, chain, 0, 4) == 2000, "idle executor: base linger");
+        CHECK(dm_plan::batch_linger_us(0, chain, 0, 4) == 0, "idle executor, no base: at once");
+        double prev = 2000;
+        for (int busy = 1; busy <= 4; busy++) {
+            const double w = dm_plan::batch_linger_us(2000, chain, busy, 4);
+            CHECK(w > prev, "busy %d: linger grows", busy);
+            prev = w;
+        }
+        const double last = dm_plan::batch_linger_us(0, chain, 3, 4);  // the last free slot of 4
+        CHECK(last > 15e3 && last < 20e3, "last free slot of 4: %.0f us (9/256 of a chain)", last);
+        CHECK(dm_plan::batch_linger_us(0, chain, 1, 32) < 50, "1 busy slot of 32: negligible");
+        CHECK(dm_plan::batch_linger_us(0, chain, 9, 4) == dm_plan::batch_linger_us(0, chain, 4, 4), "busy capped");
+    }
     if (failures) {
         std::fprintf(stderr, "%d failure(s)\n", failures);
         return 1;
