@@ -51,6 +51,7 @@ struct dm_batcher {
     std::deque<BatchReq*> q;
     uint64_t q_leaves = 0;   // leaves queued
     int busy = 0;            // slots running a batch
+    int nslots = 0;          // worker slots (set before any worker starts)
     bool stop = false;
     uint64_t n_req = 0, n_batch = 0, max_batch = 0;
 };
@@ -128,7 +129,7 @@ void batcher_worker(dm_batcher* b, size_t slot) {
                         longest = std::max(longest, b->mode == DM_BATCH_PROCESS ? b->unit : std::min(r->len, b->unit));
                     chain_us = (double)ceil_div(longest + 9, 64) * dm_plan::chain_ns_per_block(dm_plan::kQuad) * 1e-3;
                 }
-                const double w = dm_plan::batch_linger_us(b->linger_us, chain_us, b->busy, (int)b->workers.size());
+                const double w = dm_plan::batch_linger_us(b->linger_us, chain_us, b->busy, b->nslots);
                 const auto until = b->q.front()->arrived + std::chrono::microseconds((int64_t)w);
                 if (std::chrono::steady_clock::now() >= until) break;
                 const int busy0 = b->busy;
@@ -268,6 +269,8 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
             b->coders.push_back(r);
         }
     }
+    b->nslots = ns;
+    b->workers.reserve(ns);
     for (int i = 0; i < ns; i++) b->workers.emplace_back(batcher_worker, b, (size_t)i);
     *out = b;
     return DM_OK;
