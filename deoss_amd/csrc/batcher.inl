@@ -12,25 +12,20 @@
 // batch runs, the next slot collects the requests that arrived meanwhile, so under load batches
 // grow to the leaf budget and the GPU runs them back to back or side by side.
 
-#include <chrono>
-#include <condition_variable>
-#include <deque>
+#include <memory>
+
+#include "batch_queue.hpp"
 
 namespace {
 
-struct BatchReq {
+struct BatchReq : dm_batch::Req {
     const void* host = nullptr;
     uint64_t len = 0;
-    uint64_t leaves = 0;            // leaves this request adds to a batch
     uint8_t* out32 = nullptr;       // root (ROOT) or fid (PROCESS)
     uint8_t* leaf_out = nullptr;    // ROOT: leaf digests (nullable)
     void* frags_out = nullptr;      // PROCESS (nullable)
     uint8_t* seg_hashes = nullptr;  // PROCESS (nullable)
     uint8_t* frag_hashes = nullptr; // PROCESS (nullable)
-    int rc = DM_OK;
-    std::string err;
-    bool done = false;
-    std::chrono::steady_clock::time_point arrived{};
 };
 
 thread_local std::string t_batcher_err;
@@ -41,19 +36,10 @@ struct dm_batcher {
     int mode = DM_BATCH_ROOT;
     uint64_t unit = 0;
     int k = 0, m = 0;
-    uint64_t max_leaves = 0, max_bytes = 0;
-    uint32_t linger_us = 0;
     std::vector<dm_ctx*> ctxs;
     std::vector<dm_rs*> coders;
     std::vector<std::thread> workers;
-    std::mutex mu;
-    std::condition_variable cv_work, cv_done;
-    std::deque<BatchReq*> q;
-    uint64_t q_leaves = 0;   // leaves queued
-    int busy = 0;            // slots running a batch
-    int nslots = 0;          // worker slots (set before any worker starts)
-    bool stop = false;
-    uint64_t n_req = 0, n_batch = 0, max_batch = 0;
+    std::unique_ptr<dm_batch::Queue> q;   // requests, batching and linger (batch_queue.hpp)
 };
 
 namespace {
@@ -113,79 +99,22 @@ int batch_process_host(dm_rs* r, const std::vector<BatchReq*>& reqs, uint64_t se
 
 void batcher_worker(dm_batcher* b, size_t slot) {
     dm_ctx* c = b->ctxs[slot];
-    for (;;) {
-        std::vector<BatchReq*> batch;
-        {
-            std::unique_lock<std::mutex> lk(b->mu);
-            b->cv_work.wait(lk, [&] { return b->stop || !b->q.empty(); });
-            if (b->q.empty()) return;   // stop requested and nothing left to drain
-            // let a burst accumulate before launching (dm_plan::batch_linger_us), re-evaluated
-            // whenever a slot frees up or the queue fills a batch
-            while (!b->stop && !b->q.empty() && b->q_leaves < b->max_leaves) {
-                double chain_us = 0;
-                if (b->busy > 0) {
-                    uint64_t longest = 0;
-                    for (const BatchReq* r : b->q)
-                        longest = std::max(longest, b->mode == DM_BATCH_PROCESS ? b->unit : std::min(r->len, b->unit));
-                    chain_us = (double)ceil_div(longest + 9, 64) * dm_plan::chain_ns_per_block(dm_plan::kQuad) * 1e-3;
-                }
-                const double w = dm_plan::batch_linger_us(b->linger_us, chain_us, b->busy, b->nslots);
-                const auto until = b->q.front()->arrived + std::chrono::microseconds((int64_t)w);
-                if (std::chrono::steady_clock::now() >= until) break;
-                const int busy0 = b->busy;
-                b->cv_work.wait_until(lk, until, [&] {
-                    return b->stop || b->q.empty() || b->q_leaves >= b->max_leaves || b->busy != busy0;
-                });
-            }
-            if (b->q.empty()) continue;    // another slot took them meanwhile
-            uint64_t leaves = 0, bytes = 0;
-            while (!b->q.empty()) {
-                BatchReq* r = b->q.front();
-                const uint64_t rb = b->mode == DM_BATCH_PROCESS ? ceil_div(r->len, b->unit) * b->unit * 3 : r->len;
-                if (!batch.empty() && (leaves + r->leaves > b->max_leaves || bytes + rb > b->max_bytes)) break;
-                batch.push_back(r);
-                leaves += r->leaves;
-                bytes += rb;
-                b->q_leaves -= r->leaves;
-                b->q.pop_front();
-            }
-            b->busy++;
-            b->n_batch++;
-            b->max_batch = std::max<uint64_t>(b->max_batch, batch.size());
-            if (!b->q.empty()) b->cv_work.notify_one();   // another slot can start on the rest
-        }
+    std::vector<dm_batch::Req*> taken;
+    std::vector<BatchReq*> batch;
+    while (b->q->take(taken)) {
+        batch.clear();
+        for (dm_batch::Req* r : taken) batch.push_back(static_cast<BatchReq*>(r));
         const int rc = b->mode == DM_BATCH_PROCESS ? batch_process_host(b->coders[slot], batch, b->unit)
                                                    : batch_roots_host(c, batch, b->unit);
-        const std::string msg = rc == DM_OK ? std::string() : c->err;
-        {
-            std::lock_guard<std::mutex> lk(b->mu);
-            b->busy--;
-            for (BatchReq* r : batch) {
-                r->rc = rc;
-                r->err = msg;
-                r->done = true;
-            }
-        }
-        b->cv_done.notify_all();
-        b->cv_work.notify_all();   // a lingering slot re-evaluates with one busy slot fewer
+        b->q->finish(taken, rc, rc == DM_OK ? std::string() : c->err);
     }
 }
 
 int batcher_submit(dm_batcher* b, BatchReq& r) {
-    {
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (b->stop) {
-            t_batcher_err = "batcher is shutting down";
-            return DM_ERR_INVALID;
-        }
-        r.arrived = std::chrono::steady_clock::now();
-        b->q.push_back(&r);
-        b->q_leaves += r.leaves;
-        b->n_req++;
+    if (!b->q->submit(r)) {
+        t_batcher_err = "batcher is shutting down";
+        return DM_ERR_INVALID;
     }
-    b->cv_work.notify_all();   // idle slots start; a lingering one re-checks the leaf budget
-    std::unique_lock<std::mutex> lk(b->mu);
-    b->cv_done.wait(lk, [&] { return r.done; });
     t_batcher_err = r.err;
     return r.rc;
 }
@@ -196,11 +125,7 @@ extern "C" {
 
 void dm_batcher_destroy(dm_batcher* b) {
     if (!b) return;
-    {
-        std::lock_guard<std::mutex> lk(b->mu);
-        b->stop = true;
-    }
-    b->cv_work.notify_all();
+    if (b->q) b->q->stop();
     for (auto& t : b->workers)
         if (t.joinable()) t.join();
     for (dm_rs* r : b->coders) dm_rs_destroy(r);
@@ -238,11 +163,6 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
     b->unit = unit;
     b->k = data_shards;
     b->m = parity_shards;
-    // default budget: half of what K1Q keeps resident (four 37 KiB workgroups x 8 leaves per CU),
-    // so two slots' batches fit side by side
-    b->max_leaves = max_leaves ? max_leaves : 4096;
-    b->max_bytes = max_bytes ? max_bytes : (16ull << 30);
-    b->linger_us = linger_us;
     // default 4 slots per GPU: each slot's context has its own hardware queue (a CU-masked lane
     // stream), so 4 batches run side by side; measured 2 / 3 / 4 / 6 / 8 slots: 0.278 / 0.370 /
     // 0.400 / 0.398 / 0.402 GiB/s of 1 MiB FullProcessing uploads, roots 8.2 (2) / 9.1 (4) / 8.4 (8)
@@ -269,8 +189,10 @@ int dm_batcher_create(const int* devs, int ndev, int mode, uint64_t unit, int da
             b->coders.push_back(r);
         }
     }
-    b->nslots = ns;
-    b->workers.reserve(ns);
+    // default budget: half of what K1Q keeps resident (four 37 KiB workgroups x 8 leaves per CU),
+    // so two slots' batches fit side by side
+    b->q.reset(new dm_batch::Queue(ns, max_leaves ? max_leaves : 4096, max_bytes ? max_bytes : (16ull << 30),
+                                   (double)linger_us, dm_plan::chain_ns_per_block(dm_plan::kQuad)));
     for (int i = 0; i < ns; i++) b->workers.emplace_back(batcher_worker, b, (size_t)i);
     *out = b;
     return DM_OK;
@@ -289,6 +211,8 @@ int dm_batcher_root(dm_batcher* b, const void* host, uint64_t len, uint8_t* leaf
     r.host = host;
     r.len = len;
     r.leaves = ceil_div(len, b->unit);
+    r.bytes = len;
+    r.chain_bytes = std::min(len, b->unit);
     r.out32 = root;
     r.leaf_out = leaf_out;
     return batcher_submit(b, r);
@@ -308,6 +232,8 @@ int dm_batcher_process(dm_batcher* b, const void* host, uint64_t len, void* frag
     r.host = host;
     r.len = len;
     r.leaves = ceil_div(len, b->unit) * (1 + (uint64_t)(b->k + b->m));
+    r.bytes = ceil_div(len, b->unit) * b->unit * 3;   // segments + parity in device memory
+    r.chain_bytes = b->unit;                          // every segment is one full chain
     r.out32 = fid;
     r.frags_out = frags_out;
     r.seg_hashes = seg_hashes;
@@ -317,10 +243,10 @@ int dm_batcher_process(dm_batcher* b, const void* host, uint64_t len, void* frag
 
 int dm_batcher_stats(dm_batcher* b, uint64_t* requests, uint64_t* batches, uint64_t* max_batch) {
     if (!b) return DM_ERR_INVALID;
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (requests) *requests = b->n_req;
-    if (batches) *batches = b->n_batch;
-    if (max_batch) *max_batch = b->max_batch;
+    const dm_batch::Stats st = b->q->stats();
+    if (requests) *requests = st.requests;
+    if (batches) *batches = st.batches;
+    if (max_batch) *max_batch = st.max_batch;
     return DM_OK;
 }
 
