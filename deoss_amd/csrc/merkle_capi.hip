@@ -61,6 +61,24 @@ void reaper_drain(Reaper* r);
 // Device memory a DevBuf growth leaves free for the HIP runtime and everything else (DevBuf::ensure).
 constexpr size_t kMallocHeadroom = 256ull << 20;
 
+// Free / total memory of device `dev` (the current device when dev < 0), whatever device the
+// calling thread has current; false (and the error cleared) when the query fails.
+inline bool free_on(int dev, size_t* fr, size_t* tot) {
+    int cur = -1;
+    if (dev >= 0 && (hipGetDevice(&cur) != hipSuccess || cur != dev)) {
+        if (hipSetDevice(dev) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+    } else {
+        cur = -1;   // already current: nothing to restore
+    }
+    const bool ok = hipMemGetInfo(fr, tot) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    if (cur >= 0) (void)hipSetDevice(cur);
+    return ok;
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
@@ -86,14 +104,10 @@ struct DevBuf {
             // out of memory while the reaper's hipFree of a large block is still pending crashed
             // inside the HSA runtime (pthread_mutex_lock; tests/test_runtime_gpu.py, round 4).
             size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr < c + kMallocHeadroom) {
+            if (free_on(dev, &fr, &tot) && fr < c + kMallocHeadroom) {
                 reaper_drain(rp);
-                if (hipMemGetInfo(&fr, &tot) == hipSuccess && fr < c + kMallocHeadroom) {
-                    (void)hipGetLastError();
-                    return hipErrorOutOfMemory;
-                }
+                if (free_on(dev, &fr, &tot) && fr < c + kMallocHeadroom) return hipErrorOutOfMemory;
             }
-            (void)hipGetLastError();
         }
         hipError_t e = hipMalloc(&p, c);
         if (e == hipErrorOutOfMemory && rp) {
