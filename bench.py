@@ -5,10 +5,13 @@ synthetic object already resident in HBM.  Weak scaling: every rank holds `--obj
 (default 8 GiB = BASELINE configs[1]); at N GPUs the object is N x 8 GiB, sharded by aligned
 chunk ranges, with one RCCL all-gather of subtree roots before rank 0's final levels.
 
-Rank 0 prints ONE JSON line.  At N = 1 it also reports: the K1 roofline (HIP events on the launch
-stream over the timed region), the CPU baseline (the oracle's faithful serial restatement of
-common/hashtree timed on this host over the same bytes), full-size parity (GPU root == CPU root),
-a chunk-size sweep and the host-buffer end-to-end rate.
+Rank 0 prints ONE JSON line on stdout, last, at most LINE_MAX_BYTES (compact_line): the headline,
+the K1 roofline (HIP events on the launch stream over the timed region), the CPU baseline (the
+oracle's faithful serial restatement of common/hashtree timed on this host over the same bytes),
+full-size parity (GPU root == CPU root), the host-buffer end-to-end rate, the strong-scaling leg at
+N > 1, and one short entry per extra config; `ok` is false if any check failed.  The full record
+(every extra's nested roofline / traffic / CPU legs, latency tables, the in-process leg) goes to the
+detail file the line names (--detail-out; default gpurun_out/bench_detail_n<N>.json).
 """
 from __future__ import annotations
 
@@ -230,7 +233,12 @@ def main() -> None:
                     help="in-process leg: seconds before the watchdog gives up on it (the line is printed anyway)")
     ap.add_argument("--inproc-devices", type=int, default=8,
                     help="--workload inprocess on one GPU: virtual devices standing in for the GPUs")
+    ap.add_argument("--detail-out", default="",
+                    help="where the full record goes (JSON); default gpurun_out/bench_detail_n<N>.json.  stdout's "
+                         "last line is the compact headline, which names this file")
+    ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling leg")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--watchdog-check", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if args.gpus > 1 and os.environ.get("WORLD_SIZE") in (None, ""):
@@ -238,6 +246,9 @@ def main() -> None:
         sys.exit(self_launch(args.gpus, sys.argv[1:]))
     if args.launch_check:
         launch_check(args)
+        return
+    if args.watchdog_check:
+        watchdog_check(args)
         return
 
     start_heartbeat()
@@ -303,6 +314,11 @@ def main() -> None:
         out["parity"]["pinned_by"] = PIN_MERKLE
     if world > 1:
         out["launch"] = launch_info(torch, dist, world, rank, local_rank, dev_index, args)
+    detail = args.detail_out or os.path.join(ROOT, "gpurun_out", f"bench_detail_n{out['n_gpus']}.json")
+    if world > 1 and not args.total_gib and not args.no_strong:
+        progress("strong-scaling leg: configs[1]'s 8 GiB object over every rank")
+        out["strong_scaling"] = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier,
+                                                   out["value"] / world)
     if world == 1 and rank == 0 and not args.no_extras:
         out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
         progress("latency block")
@@ -325,17 +341,59 @@ def main() -> None:
         dist.all_reduce(flag, group=wait_group)           # doubles as the barrier
         if rank == 0:
             out.setdefault("other_configs", {})["in_process"] = inproc
-        if int(flag.item()):   # the leg never returned (its thread may hold GPUs): print, then every rank exits
-            if rank == 0:
-                print(json.dumps(out), flush=True)
-            sys.stdout.flush()
-            sys.stderr.flush()
-            os._exit(0)
+        if int(flag.item()):
+            exit_after_hang(out if rank == 0 else None, detail)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out, detail)
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+def exit_after_hang(out, detail):
+    """A watchdogged leg never returned (its thread may still hold GPUs or an RCCL init): rank 0
+    prints the line (ok false, the leg's error in it), then every rank leaves at once with status 3
+    -- never 0, so the driver records the hang as a failure.  No re-exec, no restart."""
+    if out is not None:
+        emit(out, detail)
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(3)
+
+
+def watchdog_check(args) -> None:
+    """Hidden --watchdog-check S (tests/test_bench_launch.py): a leg that sleeps past its S-second
+    watchdog goes through the same exit path as the N = 8 in-process leg -- no GPU touched."""
+    out = {"metric": "watchdog check", "value": 0.0, "unit": "GiB/s", "n_gpus": 1, "steps": 0, "warmup": 0}
+    r, hung = run_with_watchdog(lambda: time.sleep(60), args.watchdog_check)
+    out["other_configs"] = {"in_process": r}
+    if hung:
+        exit_after_hang(out, args.detail_out)
+    emit(out, args.detail_out)
+
+
+def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu):
+    """N > 1: BASELINE configs[1]'s one 8 GiB object sharded over all N ranks (total work fixed),
+    beside the weak-scaling headline.  At 32 MiB chunks the object is 256 leaves: one GPU already
+    runs all 256 serial chains at once (0.49 s each), so splitting them over N GPUs cannot shorten
+    the step -- strong scaling is ~1x by construction; this measures it.  Checked:
+    the sharded root against the single-GPU root and the CPU restatement of the same bytes."""
+    import copy
+    ns = copy.copy(args)
+    ns.total_gib, ns.steps, ns.warmup, ns.no_extras = 8.0, 3, 1, True
+    t0 = time.perf_counter()
+    try:
+        r = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
+    except Exception as e:   # reported, never fatal to the headline line
+        return {"error": f"{type(e).__name__}: {e}"}
+    par = r.get("parity") or {}
+    res = {"workload": "configs[1] strong: one 8 GiB object (256 leaves of 32 MiB) over "
+                       f"{world} GPUs", "value": r["value"], "unit": "GiB/s", "ms_per_step": r["ms_per_step"],
+           "steps": ns.steps, "bit_exact": par.get("bit_exact"),
+           "speedup_vs_one_gpu_share_of_weak": round(r["value"] / weak_per_gpu, 3) if weak_per_gpu else None,
+           "note": "~1x by construction at 32 MiB chunks: 256 chains of ~0.49 s run concurrently on one GPU already",
+           "wall_s": round(time.perf_counter() - t0, 2)}
+    return res
 
 
 def run_with_watchdog(fn, timeout_s):
@@ -1107,6 +1165,201 @@ def _summary(r):
     if "cpu_baseline" in r:
         keep["cpu_baseline"] = r["cpu_baseline"]
     return keep
+
+
+LINE_MAX_BYTES = 6144   # the last stdout line; the driver lost r04's 28 KB line
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data")
+
+
+def _r(x, nd=4):
+    return round(x, nd) if isinstance(x, float) else x
+
+
+def _short(s, n):
+    return s if not isinstance(s, str) or len(s) <= n else s[:n - 3] + "..."
+
+
+def _extra_line(r):
+    """One extra (a BASELINE config or entry point measured beside the headline) in a few fields:
+    its value, the time of one step, bit-exactness, its roofline fraction and bound, and ok."""
+    if not isinstance(r, dict):
+        return {"ok": False, "error": "no result"}
+    if "error" in r or "skipped" in r:
+        e = {"ok": "skipped" in r and "error" not in r}
+        e["error" if "error" in r else "skipped"] = _short(r.get("error") or r.get("skipped"), 160)
+        return e
+    rf = r.get("roofline") if isinstance(r.get("roofline"), dict) else {}
+    e = {"value": _r(r.get("value")), "unit": r.get("unit"), "ms": _r(r.get("ms_per_step"), 2),
+         "bit_exact": r.get("bit_exact")}
+    if rf:
+        e.update({"bound": rf.get("bound"), "frac": _r(rf.get("frac"), 6)})
+        if rf.get("traffic_over_algorithmic") is not None:
+            e["traffic_x"] = rf["traffic_over_algorithmic"]
+    cb = r.get("cpu_baseline")
+    if isinstance(cb, dict) and cb.get("value") is not None:
+        e["cpu"] = {"value": _r(cb["value"]), "cores": cb.get("cores")}
+    e["ok"] = e["bit_exact"] is True
+    return e
+
+
+def _in_process_line(r):
+    if not isinstance(r, dict):
+        return {"ok": False, "error": "no result"}
+    if "error" in r or "skipped" in r:
+        return {"ok": "error" not in r, **{k: _short(r[k], 160) for k in ("error", "skipped") if k in r}}
+    e = {"devices": r.get("devices"), "virtual": r.get("virtual_devices"), "bit_exact": r.get("bit_exact")}
+    for leg in ("sharded_object", "batch_by_objects", "concurrent_calls"):
+        v = r.get(leg) or {}
+        e[leg] = ({"GiBps": v.get("GiBps"), "bit_exact": (v.get("parity") or {}).get("bit_exact")}
+                  if "error" not in v else {"error": _short(v["error"], 120)})
+    x = (r.get("sharded_object") or {}).get("exchange") or {}
+    if x:
+        e["exchange_avg_us"] = x.get("avg_us")
+    e["ok"] = r.get("bit_exact") is True
+    return e
+
+
+def compact_line(out, detail_path=None):
+    """Rank 0's last stdout line, at most LINE_MAX_BYTES: the headline and its evidence (roofline,
+    CPU baseline, parity, host-buffer rate, launch at N > 1) plus one short entry per extra.  The
+    full record (every extra's nested roofline, traffic and CPU legs, the latency tables, the
+    in-process leg) goes to the detail file this line names.  `ok` is false when any parity check
+    failed or any extra / leg errored; `problems` says which."""
+    line = {k: _r(out[k]) for k in HEAD_KEYS if k in out}
+    cfg = out.get("config") or {}
+    line["config"] = {k: cfg[k] for k in ("workload", "object_bytes", "chunk", "leaves", "parallelism") if k in cfg}
+    line["config"]["workload"] = _short(cfg.get("workload"), 240)
+    problems = []
+    rf = out.get("roofline") or {}
+    if rf:
+        roof = {k: _r(rf.get(k), 6) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic") if k in rf}
+        kn = rf.get("kernel") or ""     # "leaf_kernel_quad (K1Q, producer/...)" -> "leaf_kernel_quad (K1Q)"
+        roof["kernel"] = kn.split(" (")[0] + (f" ({kn.split(' (')[1].split(',')[0].rstrip(')')})" if " (" in kn else "")
+        alg = rf.get("algorithmic_bytes_per_launch")
+        roof.update({"algorithmic_bytes_per_launch": alg, "k1_avg_ms": rf.get("k1_avg_ms"),
+                     "k1_launches": rf.get("k1_launches")})
+        if rf.get("traffic") and alg:
+            roof["traffic_over_algorithmic"] = round(rf["traffic"] / alg, 5)
+        cf = rf.get("chain_issue_floor") or {}
+        if cf:
+            roof["chain_issue_floor"] = {"floor_ms": cf.get("floor_ms"), "frac": cf.get("frac"),
+                                         "valu_per_block": cf.get("valu_per_block_on_chain")}
+        mp = rf.get("measured_read_peak") or {}
+        if mp:
+            roof["measured_read_peak_GBps"] = mp.get("GBps")
+        line["roofline"] = roof
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c = {k: _r(cb.get(k)) for k in ("value", "unit", "cores", "kind") if k in cb}
+        c["sample"] = _short(cb.get("sample"), 200)
+        par = cb.get("parallel") or {}
+        if par:
+            c["parallel"] = {"value": par.get("value"), "cores": par.get("cores")}
+        est = cb.get("all_physical_cores_estimate") or {}
+        if est.get("value"):
+            c["all_cores_estimate"] = {"value": est.get("value"), "cores": est.get("cores")}
+        host = cb.get("host") or {}
+        if host.get("model"):
+            c["host"] = _short(host["model"], 60)
+        line["cpu_baseline"] = c
+    for k in ("vs_cpu_share",):
+        if k in out:
+            line[k] = out[k]
+    if out.get("vs_baseline_basis"):
+        line["vs_baseline_basis"] = _short(out["vs_baseline_basis"], 200)
+    par = out.get("parity")
+    if isinstance(par, dict):
+        p = {k: par[k] for k in ("bit_exact", "prefix_bit_exact", "cpu_bit_exact", "gpu_root", "cpu_root",
+                                 "sharded_root", "prefix_bytes", "cpu_threads", "cpu_root_gibs") if k in par}
+        line["parity"] = p
+        if par.get("bit_exact") is not True:
+            problems.append("parity")
+    elif out.get("root"):
+        line["root"] = out["root"]
+    e2e = out.get("e2e")
+    if isinstance(e2e, dict):
+        line["e2e"] = {k: e2e[k] for k in ("pinned_host_gibs", "pageable_host_gibs", "root_matches") if k in e2e}
+        if e2e.get("root_matches") is False:
+            problems.append("e2e")
+    sw = out.get("sweep")
+    if isinstance(sw, list) and sw:
+        line["sweep_gibs"] = {str(s.get("chunk")): s.get("gibs") for s in sw}
+        if any(s.get("bit_exact") is False for s in sw):
+            problems.append("sweep")
+    la = out.get("launch")
+    if isinstance(la, dict):
+        line["launch"] = {k: la.get(k) for k in ("world_size", "backend", "device_count", "distinct_gpus",
+                                                 "rccl_version", "launcher")}
+        line["launch"]["launcher"] = _short(la.get("launcher"), 60)
+    for k in ("same_device", "note", "ranks"):
+        if k in out:
+            line[k] = out[k]
+    st = out.get("strong_scaling")
+    if isinstance(st, dict):
+        line["strong_scaling"] = st
+        if st.get("bit_exact") is False or "error" in st:
+            problems.append("strong_scaling")
+    extras = {}
+    for name, r in (out.get("other_configs") or {}).items():
+        extras[name] = _in_process_line(r) if name == "in_process" else _extra_line(r)
+        if not extras[name].get("ok"):
+            problems.append(name)
+    if extras:
+        line["extras"] = extras
+    lat = out.get("latency")
+    if isinstance(lat, dict):
+        lt = {}
+        for k, v in lat.items():
+            if not isinstance(v, dict) or k == "pinned_by":
+                continue
+            if "error" in v:
+                lt[k] = {"error": _short(v["error"], 100)}
+            elif k.startswith("crossover"):
+                lt[k] = {"gpu_faster_from": v.get("gpu_faster_from"), "bit_exact": v.get("bit_exact")}
+            elif "gpu" in v:
+                lt[k] = {"gpu_p50_ms": v["gpu"].get("p50_ms"), "cpu_p50_ms": v.get("cpu_1core", {}).get("p50_ms"),
+                         "bit_exact": v.get("bit_exact")}
+        lt["bit_exact"] = lat.get("bit_exact")
+        line["latency"] = lt
+        if lat.get("bit_exact") is not True:
+            problems.append("latency")
+    line["ok"] = not problems
+    if problems:
+        line["problems"] = problems
+    line["detail"] = detail_path
+    # last resort: never let the line outgrow the bound (drop the least important blocks first)
+    for k in ("sweep_gibs", "latency", "vs_baseline_basis"):
+        if len(json.dumps(line, separators=(",", ":"))) <= LINE_MAX_BYTES:
+            break
+        line.pop(k, None)
+    if len(json.dumps(line, separators=(",", ":"))) > LINE_MAX_BYTES and "extras" in line:
+        line["extras"] = {k: {"ok": v.get("ok"), "value": v.get("value")} for k, v in line["extras"].items()}
+    return line
+
+
+def write_detail(out, path):
+    """The full record of the run (everything compact_line leaves out) as JSON at `path`; the path
+    written, or None when it could not be written (the line says so, the run goes on)."""
+    if not path:
+        return None
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return os.path.relpath(os.path.abspath(path), ROOT) if os.path.abspath(path).startswith(ROOT) else path
+    except OSError as e:
+        print(f"[bench] detail file {path}: {e}", file=sys.stderr, flush=True)
+        return None
+
+
+def emit(out, detail_path):
+    """Rank 0: write the detail file, then print the compact line as stdout's last line."""
+    where = write_detail(out, detail_path)
+    line = compact_line(out, where)
+    print(json.dumps(line, separators=(",", ":")), flush=True)
+    return line
 
 
 def measure_read_peak(ctx, torch, buf, nbytes, sptr, stream, reps=5):

@@ -5,8 +5,8 @@
 // Callers block in submit() until a worker has run their request.  Workers (one per slot) block
 // in take(), which returns the next batch: everything queued, oldest first, up to the leaf and
 // byte budgets, after holding a burst open for dm_plan::batch_linger_us from the oldest request's
-// arrival.  That wait is re-evaluated whenever a slot finishes (the busy count changes) or the
-// queue fills a batch, and it ends at once on stop().  finish() hands a batch's result back to
+// arrival.  That wait is re-evaluated whenever a slot finishes (the busy count changes), and it
+// ends at once when the queue holds a full batch by either budget (leaves or bytes) or on stop().  finish() hands a batch's result back to
 // its callers.  After stop(), take() drains what is queued and then returns false; submit()
 // refuses new requests.
 #pragma once
@@ -55,6 +55,7 @@ class Queue {
             r.arrived = std::chrono::steady_clock::now();
             q_.push_back(&r);
             q_leaves_ += r.leaves;
+            q_bytes_ += r.bytes;
             st_.requests++;
         }
         cv_work_.notify_all();   // idle slots start; a lingering one re-checks the budget
@@ -70,7 +71,7 @@ class Queue {
         for (;;) {
             cv_work_.wait(lk, [&] { return stop_ || !q_.empty(); });
             if (q_.empty()) return false;   // stop requested and nothing left to drain
-            while (!stop_ && !q_.empty() && q_leaves_ < max_leaves_) {
+            while (!stop_ && !q_.empty() && !full()) {
                 double chain_us = 0;
                 if (busy_ > 0) {
                     uint64_t longest = 0;
@@ -82,7 +83,7 @@ class Queue {
                 if (std::chrono::steady_clock::now() >= until) break;
                 const int busy0 = busy_;
                 cv_work_.wait_until(lk, until, [&] {
-                    return stop_ || q_.empty() || q_leaves_ >= max_leaves_ || busy_ != busy0;
+                    return stop_ || q_.empty() || full() || busy_ != busy0;
                 });
             }
             if (!q_.empty()) break;   // else another slot took them meanwhile
@@ -95,6 +96,7 @@ class Queue {
             leaves += r->leaves;
             bytes += r->bytes;
             q_leaves_ -= r->leaves;
+            q_bytes_ -= r->bytes;
             q_.pop_front();
         }
         busy_++;
@@ -133,6 +135,9 @@ class Queue {
     }
 
   private:
+    // a whole batch's worth is queued (either budget reached): the linger ends, the batch launches
+    bool full() const { return q_leaves_ >= max_leaves_ || q_bytes_ >= max_bytes_; }
+
     const int nslots_;
     const uint64_t max_leaves_, max_bytes_;
     const double linger_us_, chain_ns_;
@@ -140,6 +145,7 @@ class Queue {
     std::condition_variable cv_work_, cv_done_;
     std::deque<Req*> q_;
     uint64_t q_leaves_ = 0;   // leaves queued
+    uint64_t q_bytes_ = 0;    // bytes queued
     int busy_ = 0;            // slots running a batch
     bool stop_ = false;
     Stats st_;

@@ -58,7 +58,7 @@ struct Reaper;
 void reaper_put(Reaper* r, int dev, void* p, bool pinned);
 void reaper_drain(Reaper* r);
 
-// Device memory a DevBuf growth leaves free for the HIP runtime and everything else (DevBuf::ensure).
+// Device memory an allocation leaves free for the HIP runtime and everything else (dev_alloc).
 constexpr size_t kMallocHeadroom = 256ull << 20;
 
 // Free / total memory of device `dev` (the current device when dev < 0), whatever device the
@@ -79,56 +79,112 @@ inline bool free_on(int dev, size_t* fr, size_t* tot) {
     return ok;
 }
 
+inline int current_device() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        d = 0;
+    }
+    return d;
+}
+
+// The process's one allocator: every hipMalloc / hipFree of device memory this library makes
+// (DevBuf growth and release, the reapers' deferred frees, every context's) runs under its HIP
+// device's mutex, and every hipHostMalloc / hipHostFree under the host mutex.  Round 4 saw four
+// segfaults inside the HSA runtime (pthread_mutex_lock under hipMalloc) when a DevBuf growth ran
+// out of memory while a reaper's hipFree of a large block was still pending behind a running
+// chain.  tools/oom_free_race.hip separates the conditions; whatever its verdict,
+// under these locks the library never has a hipMalloc in flight beside one of its own hipFrees on
+// that device, and dev_alloc never issues a hipMalloc that hipMemGetInfo says cannot succeed --
+// not on the first try and not on the retry after a reaper drain.  The cost: an allocation waits
+// behind a reaper free of the same device, which waits for the device's queued work (growth only;
+// steady-state calls reuse their buffers and allocate nothing).
+struct AllocLocks {
+    static constexpr int kDevs = 64;
+    std::mutex dev[kDevs];
+    std::mutex host;
+};
+AllocLocks& alloc_locks() {
+    static AllocLocks* a = new AllocLocks();   // never destroyed: reapers may free during exit
+    return *a;
+}
+std::mutex& dev_mutex(int dev) { return alloc_locks().dev[(unsigned)dev % AllocLocks::kDevs]; }
+
+// hipMalloc(n) on device `dev` (current on the calling thread), or hipErrorOutOfMemory without
+// calling hipMalloc when less than n + kMallocHeadroom is free.
+hipError_t dev_alloc(int dev, void** p, size_t n) {
+    *p = nullptr;
+    std::lock_guard<std::mutex> lk(dev_mutex(dev));
+    size_t fr = 0, tot = 0;
+    if (free_on(dev, &fr, &tot) && fr < n + kMallocHeadroom) return hipErrorOutOfMemory;
+    hipError_t e = hipMalloc(p, n);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+    }
+    return e;
+}
+
+void dev_release(int dev, void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(dev_mutex(dev));
+    (void)hipFree(p);   // waits for the device's queued work
+    (void)hipGetLastError();
+}
+
+hipError_t host_alloc(void** p, size_t n, unsigned flags) {
+    *p = nullptr;
+    std::lock_guard<std::mutex> lk(alloc_locks().host);
+    hipError_t e = hipHostMalloc(p, n, flags);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        *p = nullptr;
+    }
+    return e;
+}
+
+void host_release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(alloc_locks().host);
+    (void)hipHostFree(p);
+    (void)hipGetLastError();
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
     Reaper* rp = nullptr;   // set (context scratch): growth hands the old buffer to the context's reaper
-    int dev = -1;
+    int dev = -1;           // HIP device (-1: the device current at each ensure / release)
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
+        const int id = dev >= 0 ? dev : current_device();
         if (p) {
             if (rp) {   // freed once the work queued so far has finished; this caller does not wait
-                reaper_put(rp, dev, p, false);
+                reaper_put(rp, id, p, false);
             } else {
                 hipError_t e = hipDeviceSynchronize();   // scratch may still be in use by queued work
                 if (e != hipSuccess) return e;
-                (void)hipFree(p);
+                dev_release(id, p);
             }
             p = nullptr;
             cap = 0;
         }
-        size_t c = round_up(std::max<size_t>(n, 4096), 2ull << 20);
-        if (rp) {
-            // Near full HBM, first let the frees already queued in the reaper happen, and do not ask
-            // hipMalloc for more than is free: measured on MI355X (ROCm 7), a hipMalloc that runs
-            // out of memory while the reaper's hipFree of a large block is still pending crashed
-            // inside the HSA runtime (pthread_mutex_lock; tests/test_runtime_gpu.py, round 4).
-            size_t fr = 0, tot = 0;
-            if (free_on(dev, &fr, &tot) && fr < c + kMallocHeadroom) {
-                reaper_drain(rp);
-                if (free_on(dev, &fr, &tot) && fr < c + kMallocHeadroom) return hipErrorOutOfMemory;
-            }
-        }
-        hipError_t e = hipMalloc(&p, c);
+        const size_t c = round_up(std::max<size_t>(n, 4096), 2ull << 20);
+        hipError_t e = dev_alloc(id, &p, c);
         if (e == hipErrorOutOfMemory && rp) {
             // the memory this growth needs may still sit in the reaper's queue (this buffer's old
             // block among it, freed only once every stream of the device has drained): wait for
-            // those frees, then try once more
-            (void)hipGetLastError();
-            p = nullptr;
+            // those frees, then try once more -- dev_alloc checks free memory again first
             reaper_drain(rp);
-            e = hipMalloc(&p, c);
+            e = dev_alloc(id, &p, c);
         }
-        if (e != hipSuccess) {
-            p = nullptr;
-            return e;
-        }
+        if (e != hipSuccess) return e;
         cap = c;
         return hipSuccess;
     }
     uint8_t* u8() { return static_cast<uint8_t*>(p); }
     void release() {
-        if (p) (void)hipFree(p);
+        dev_release(dev >= 0 ? dev : current_device(), p);
         p = nullptr;
         cap = 0;
     }
@@ -139,17 +195,17 @@ struct PinnedBuf {
     size_t cap = 0;
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
-        if (p) (void)hipHostFree(p);
+        host_release(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        hipError_t e = host_alloc(&p, n, hipHostMallocDefault);
         if (e != hipSuccess) return e;
         cap = n;
         return hipSuccess;
     }
     uint8_t* u8() { return static_cast<uint8_t*>(p); }
     void release() {
-        if (p) (void)hipHostFree(p);
+        host_release(p);
         p = nullptr;
         cap = 0;
     }
@@ -205,8 +261,8 @@ struct Reaper {
                 active++;
             }
             if (hipSetDevice(it.dev) == hipSuccess) {
-                if (it.pinned) (void)hipHostFree(it.p);
-                else (void)hipFree(it.p);
+                if (it.pinned) host_release(it.p);
+                else dev_release(it.dev, it.p);
             }
             (void)hipGetLastError();
             {
@@ -311,6 +367,7 @@ struct dm_ctx {
     // compaction and the batch split run with G = N on a one-GPU box.  RCCL rejects duplicate
     // GPUs, so the gather of subtree roots is then a D2D copy to device 0 (real GPUs: RCCL).
     bool virtual_devs = false;
+    bool keep_claimed = false;             // its lanes' keep bytes count in g_keep_claimed (dm_create)
     // Exchange timing of multi-device calls while timing is on (dm_exchange_timing): host clock
     // from every device's subtree roots being ready to the gathered slots being on every device.
     std::mutex xmu;
@@ -580,12 +637,12 @@ uint8_t* kit_table(dm_ctx* c, int dev, StreamKit* k, uint64_t bytes) {
 }
 
 // Grow a pinned buffer to n bytes without waiting on the device: the old one goes to the reaper.
+// Both attempts go through host_alloc (under the host allocation lock).
 hipError_t pinned_grow(dm_ctx* c, int dev, PinnedBuf& b, uint64_t n) {
     if (n <= b.cap) return hipSuccess;
     c->reaper.put(dev, b);
     hipError_t e = b.ensure(n);
     if (e == hipErrorOutOfMemory) {   // the old buffer may still be queued: free it, retry once
-        (void)hipGetLastError();
         c->reaper.drain();
         e = b.ensure(n);
     }
@@ -1493,30 +1550,47 @@ int dm_host_alloc(uint64_t bytes, void** out) {
     if (!out || bytes == 0) return bad_arg();
     *out = nullptr;
     DeviceRestore dev;
-    const hipError_t e = hipHostMalloc(out, bytes, hipHostMallocPortable);
+    const hipError_t e = host_alloc(out, bytes, hipHostMallocPortable);
     if (e != hipSuccess) {
         *out = nullptr;
-        (void)hipGetLastError();
         return set_err(e == hipErrorOutOfMemory ? DM_ERR_NOMEM : DM_ERR_HIP, "dm_host_alloc: hipHostMalloc failed");
     }
     return DM_OK;
 }
 
-void dm_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
-}
+void dm_host_free(void* p) { host_release(p); }
 
 }  // extern "C"
 
 namespace {
 
+// Object-buffer bytes every live context of this process may keep idle on each HIP device (lanes
+// x keep_bytes per GPU of the context), claimed at dm_create and returned at dm_destroy, so the
+// default lane count is sized per GPU, not per context: the Go hashtree context, the
+// process context and any other dm_ctx on the same GPU share one budget.
+std::mutex g_keep_mu;
+std::map<int, uint64_t> g_keep_claimed;
+
+uint64_t keep_claimed(int dev) {
+    std::lock_guard<std::mutex> lk(g_keep_mu);
+    auto it = g_keep_claimed.find(dev);
+    return it == g_keep_claimed.end() ? 0 : it->second;
+}
+
+void keep_claim(int dev, int64_t delta) {
+    std::lock_guard<std::mutex> lk(g_keep_mu);
+    uint64_t& v = g_keep_claimed[dev];
+    v = delta < 0 && (uint64_t)(-delta) > v ? 0 : v + delta;
+}
+
 // Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else sized from the
-// first GPU's free HBM.  Every lane runs on a hardware queue of its own (init_device), so L lanes
+// first GPU's HBM.  Every lane runs on a hardware queue of its own (init_device), so L lanes
 // overlap L large calls (measured: 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound
 // at 4 for pinned 8 GiB ones; tools/lanes_probe.py, profiles/r03/LOGS.md#r03w_lanes.log).  What a lane
 // costs while idle is the object buffer it keeps between calls, at most kLaneKeepBytes (16 GiB),
-// so the default is as many lanes (up to 4) as keep at most half of the free HBM idle: 4 on an
-// MI355X (288 GB), fewer on a GPU with little free memory.
+// so the default is as many lanes (1 to 4) as keep (a) at most half of the free HBM idle and (b),
+// together with every other live context's claim on this GPU, at most half of the GPU's HBM:
+// 4 for the first two default contexts on an MI355X (288 GB), then 1.
 int default_lanes(int dev) {
     const char* v = std::getenv("DEOSS_LANES");
     if (v && *v) return std::min(std::max(std::atoi(v), 1), kMaxLanes);
@@ -1525,8 +1599,10 @@ int default_lanes(int dev) {
         (void)hipGetLastError();
         return 2;
     }
-    const uint64_t by_hbm = (uint64_t)free_b / (2 * kLaneKeepBytes);
-    return (int)std::min<uint64_t>(std::max<uint64_t>(by_hbm, 1), 4);
+    const uint64_t by_free = (uint64_t)free_b / (2 * kLaneKeepBytes);
+    const uint64_t half = (uint64_t)total_b / 2, claimed = keep_claimed(dev);
+    const uint64_t by_budget = claimed >= half ? 0 : (half - claimed) / kLaneKeepBytes;
+    return (int)std::min<uint64_t>(std::max<uint64_t>(std::min(by_free, by_budget), 1), 4);
 }
 
 int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
@@ -1564,6 +1640,8 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
             return rc;
         }
     }
+    for (const Dev& d : c->devs) keep_claim(d.id, (int64_t)d.keep_bytes);   // returned by dm_destroy
+    c->keep_claimed = true;
     const char* fs = std::getenv("DEOSS_FORCE_SHARDED");
     c->force_sharded = fs != nullptr && fs[0] == '1';
     c->virtual_devs = nvirt > 1;
@@ -1605,7 +1683,10 @@ void dm_destroy(dm_ctx* ctx) {
         ctx->slots[g].kits.clear();
     }
     ctx->reaper.finish();
-    for (auto& d : ctx->devs) destroy_device(d);
+    for (auto& d : ctx->devs) {
+        if (ctx->keep_claimed) keep_claim(d.id, -(int64_t)d.keep_bytes);
+        destroy_device(d);
+    }
     delete ctx;
 }
 

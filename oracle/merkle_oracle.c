@@ -281,12 +281,13 @@ void or_fill_splitmix(void *dst, uint64_t off, uint64_t nbytes, uint64_t seed) {
 }
 
 /* ---- root of a synthetic object that never exists in memory as a whole ----
- * The object is bytes [0, len) of the splitmix64 stream `seed` (len a multiple of 8), split into
+ * The object is bytes [base, base + len) of the splitmix64 stream `seed` (base and len multiples
+ * of 8; base 0 but for one GPU's share of a larger object, or_root_synthetic_at), split into
  * `chunk`-byte leaves (chunk a multiple of 64).  Each thread takes whole leaves (atomic counter),
  * regenerates a leaf's bytes 1 MiB at a time into its own buffer and feeds them to the compression
  * function, so a 1 TiB object (BASELINE configs[3]) is checked with nthreads x 1 MiB of memory. */
 typedef struct {
-    uint64_t len, chunk, seed, n;
+    uint64_t base, len, chunk, seed, n;
     uint64_t next;           /* next leaf to take (atomic) */
     uint8_t *leaf;
 } synth_job;
@@ -299,14 +300,14 @@ static void synth_leaf(const synth_job *j, uint64_t i, uint8_t *buf, uint64_t bu
     uint64_t done = 0;
     while (done + 64 <= l) {   /* whole blocks, bufsz (a multiple of 64) at a time */
         uint64_t take = l - done < bufsz ? (l - done) / 64 * 64 : bufsz;
-        or_fill_splitmix(buf, b0 + done, take, j->seed);
+        or_fill_splitmix(buf, j->base + b0 + done, take, j->seed);
         compress(st, buf, take / 64);
         done += take;
     }
     uint8_t tail[128];
     const uint64_t r = l - done;   /* < 64, a multiple of 8 */
     memset(tail, 0, sizeof tail);
-    if (r) or_fill_splitmix(tail, b0 + done, r, j->seed);
+    if (r) or_fill_splitmix(tail, j->base + b0 + done, r, j->seed);
     tail[r] = 0x80;
     const uint64_t tb = (r + 9 <= 64) ? 64 : 128, bits = l * 8;
     for (int k = 0; k < 8; k++) tail[tb - 1 - k] = (uint8_t)(bits >> (8 * k));
@@ -331,12 +332,14 @@ static void *synth_worker(void *arg) {
     return NULL;
 }
 
-/* Returns -1 for len 0, -2 for a bad chunk/len, else 0; leaf_out (nullable) gets n x 32 bytes. */
-int or_root_synthetic(uint64_t len, uint64_t chunk, uint64_t seed, uint8_t *leaf_out, uint8_t root[32],
-                      int nthreads) {
+/* Root of the tree over bytes [base, base + len) of the stream: one GPU's share of a larger object
+ * (configs[3]: 4,096 leaves at base = rank x 128 GiB), whose subtree root the device computes.
+ * Returns -1 for len 0, -2 for a bad chunk/len/base, else 0; leaf_out (nullable) gets n x 32 bytes. */
+int or_root_synthetic_at(uint64_t base, uint64_t len, uint64_t chunk, uint64_t seed, uint8_t *leaf_out,
+                         uint8_t root[32], int nthreads) {
     if (len == 0) return -1;
-    if (chunk == 0 || chunk % 64 || len % 8) return -2;
-    synth_job j = {len, chunk, seed, (len + chunk - 1) / chunk, 0, NULL};
+    if (chunk == 0 || chunk % 64 || len % 8 || base % 8) return -2;
+    synth_job j = {base, len, chunk, seed, (len + chunk - 1) / chunk, 0, NULL};
     j.leaf = leaf_out ? leaf_out : (uint8_t *)malloc(32 * j.n);
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
@@ -350,4 +353,10 @@ int or_root_synthetic(uint64_t len, uint64_t chunk, uint64_t seed, uint8_t *leaf
     free(tmp);
     if (!leaf_out) free(j.leaf);
     return 0;
+}
+
+/* Returns -1 for len 0, -2 for a bad chunk/len, else 0; leaf_out (nullable) gets n x 32 bytes. */
+int or_root_synthetic(uint64_t len, uint64_t chunk, uint64_t seed, uint8_t *leaf_out, uint8_t root[32],
+                      int nthreads) {
+    return or_root_synthetic_at(0, len, chunk, seed, leaf_out, root, nthreads);
 }

@@ -308,6 +308,7 @@ class Oracle:
         L.or_root_buffer.argtypes = [vp, u64, u64, vp, vp, ctypes.c_int]
         L.or_fill_splitmix.argtypes = [vp, u64, u64, u64]
         L.or_root_synthetic.argtypes = [u64, u64, u64, vp, vp, ctypes.c_int]
+        L.or_root_synthetic_at.argtypes = [u64, u64, u64, u64, vp, vp, ctypes.c_int]
         L.or_set_backend.argtypes = [ctypes.c_int]
         L.or_rs_matrix.argtypes = [ctypes.c_int, ctypes.c_int, vp]
         L.or_rs_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -370,13 +371,13 @@ class Oracle:
         return leaves, root
 
     def root_synthetic(self, length: int, chunk: int, seed: int, nthreads: int = 1,
-                       want_leaves: bool = False) -> Tuple[Optional[bytes], bytes]:
-        """Root of bytes [0, length) of the splitmix64 stream `seed`, regenerated leaf by leaf
-        (no whole-object buffer: the 1 TiB configs[3] check)."""
+                       want_leaves: bool = False, base: int = 0) -> Tuple[Optional[bytes], bytes]:
+        """Root of bytes [base, base + length) of the splitmix64 stream `seed`, regenerated leaf by
+        leaf (no whole-object buffer: the 1 TiB configs[3] check; base > 0: one GPU's share)."""
         n = (length + chunk - 1) // chunk if length else 0
         leaf = ctypes.create_string_buffer(max(32 * n, 32)) if want_leaves else None
         root = ctypes.create_string_buffer(32)
-        rc = self.L.or_root_synthetic(length, chunk, seed, leaf, root, nthreads)
+        rc = self.L.or_root_synthetic_at(base, length, chunk, seed, leaf, root, nthreads)
         if rc == -1:
             raise ValueError("Empty data")
         if rc != 0:

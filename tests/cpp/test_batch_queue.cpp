@@ -6,6 +6,7 @@
 //  - a burst that starts while other slots are busy is held open (busy-scaled linger), so a burst
 //    trickling in over a few ms is not cut into one batch per free slot;
 //  - a queue whose oldest request has already waited launches at once;
+//  - a queue that holds a full batch by the byte budget (leaves to spare) launches at once;
 //  - stop() drains what is queued, then refuses new requests.
 #include <atomic>
 #include <chrono>
@@ -175,6 +176,39 @@ static void test_old_queue_launches_at_once() {
     pool.join();
 }
 
+// the byte budget ends the linger too: one slot busy, a 40 ms base linger, and four
+// 1 MiB requests that fill the 4 MiB byte budget with 4 of 4096 leaves: the free slot launches
+// them at once instead of holding the burst open
+static void test_byte_budget_ends_linger() {
+    dm_batch::Queue q(2, 4096, 4ull << 20, 40000, 936.0);
+    Pool pool(q, 2, 100000);                // a batch "runs" 100 ms
+    TReq first;
+    first.id = 1;
+    first.leaves = 1;
+    first.bytes = 1;
+    first.chain_bytes = 32 << 20;
+    std::thread t1([&] { q.submit(first); });
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));   // first: 40 ms linger, then running
+    std::vector<TReq> full(4);
+    std::vector<std::thread> th;
+    const auto t0 = clk::now();
+    for (int i = 0; i < 4; i++) {
+        full[i].id = 10 + i;
+        full[i].leaves = 1;
+        full[i].bytes = 1 << 20;
+        full[i].chain_bytes = 32 << 20;
+        th.emplace_back([&, i] { q.submit(full[i]); });
+    }
+    for (auto& t : th) t.join();
+    const double ms = ms_since(t0);
+    t1.join();
+    // launched at once: ~100 ms of "run"; a linger of 40 ms + the busy-scaled chain term would add >= 40
+    EXPECT(ms < 135, "a byte-full batch took %.1f ms", ms);
+    const dm_batch::Stats st = q.stats();
+    EXPECT(st.batches == 2, "expected 2 batches, got %llu", (unsigned long long)st.batches);
+    pool.join();
+}
+
 static void test_stop_drains() {
     dm_batch::Queue q(2, 4096, 1ull << 40, 0, 936.0);
     std::vector<TReq> reqs(16);
@@ -199,6 +233,7 @@ int main() {
     test_idle_launch();
     test_burst_while_busy();
     test_old_queue_launches_at_once();
+    test_byte_budget_ends_linger();
     test_stop_drains();
     if (fails) {
         std::fprintf(stderr, "%d failure(s)\n", fails);

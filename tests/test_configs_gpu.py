@@ -1,0 +1,125 @@
+"""BASELINE configs[2], configs[4] and one GPU's share of configs[3] at their full workloads, every
+root checked against the CPU oracle (until round 4 these shapes ran only in
+bench.py).  The oracle is the checker only; every result comes from libdeoss_merkle.so.
+
+  configs[2]  4,096 x 4 MiB objects resident in HBM, one root each (dm_root_batch_device_async):
+              many independent trees of one 4 MiB leaf (chunk 32 MiB), root = SHA256(h || h).
+  configs[4]  one GPU's share of 100,000 x 1 MiB host objects: 12,500 x 1 MiB in pinned host
+              memory through dm_root_batch (the upload regime: host buffers in, roots out).
+  configs[3]  one GPU's share of the 1 TiB object: 4,096 x 32 MiB leaves (128 GiB) generated in
+              HBM at the share's byte offset, reduced 12 levels by dm_subtree_device_async (the
+              block root that rank sends in the RCCL all-gather), against the oracle's root of
+              the same leaf range regenerated leaf by leaf (or_root_synthetic_at).
+
+Reference path: /root/reference/common/hashtree/types.go:19-39 (NewHashTree: one merkletree per
+object, types.go:38), hashtree.go:23-30 (leaf = SHA-256 of the chunk)."""
+import hashlib
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0xDE0550000          # configs k use seed 0xDE0550000 + k
+MiB, GiB = 1 << 20, 1 << 30
+CHUNK = 32 * MiB
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _threads():
+    """The job's CPU share (16 on the GPU box; os.cpu_count() there is the whole machine)."""
+    for v in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        x = os.environ.get(v, "")
+        if x.isdigit() and int(x) > 0:
+            return int(x)
+    return min(16, os.cpu_count() or 1)
+
+
+def _need_hbm(torch, nbytes):
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    assert free >= nbytes, f"{free} B of HBM free, the workload needs {nbytes} B"
+
+
+def test_configs2_4096x4MiB_device_batch(ctx, oracle_lib):
+    from concurrent.futures import ThreadPoolExecutor
+    torch = _torch()
+    nobj, obj = 4096, 4 * MiB
+    seed0 = SEED + 2
+    _need_hbm(torch, nobj * obj + 4 * GiB)
+    buf = torch.empty(nobj * obj, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for j in range(nobj):                                     # object j: splitmix64 stream seed0 + j
+        ctx.fill_synthetic_async(buf.data_ptr() + j * obj, 0, obj, seed0 + j, s)
+    roots = torch.zeros(32 * nobj, dtype=torch.uint8, device="cuda")
+    ctx.root_batch_device_async([buf.data_ptr() + j * obj for j in range(nobj)], [obj] * nobj, CHUNK,
+                                roots.data_ptr(), s)
+    torch.cuda.synchronize()
+    got = bytes(roots.cpu().numpy())
+    host = torch.empty(nobj * obj, dtype=torch.uint8, pin_memory=True)
+    host.copy_(buf)
+    del buf
+    torch.cuda.empty_cache()
+    hv = host.numpy()
+    for j in (0, 1777, nobj - 1):                             # the device generator == the oracle's
+        assert bytes(hv[j * obj:(j + 1) * obj]) == oracle_lib.splitmix_bytes(obj, seed0 + j), j
+    base = host.data_ptr()
+    with ThreadPoolExecutor(_threads()) as ex:
+        wants = list(ex.map(lambda j: oracle_lib.root_buffer_ptr(base + j * obj, obj, CHUNK)[1], range(nobj)))
+    bad = [j for j in range(nobj) if got[32 * j:32 * j + 32] != wants[j]]
+    assert not bad, f"{len(bad)} of {nobj} roots differ, first {bad[:5]}"
+    # one object, one leaf: root = SHA256(leaf || leaf) (merkletree v0.2.0's single-leaf rule)
+    leaf = hashlib.sha256(bytes(hv[:obj])).digest()
+    assert got[:32] == hashlib.sha256(leaf + leaf).digest()
+
+
+def test_configs4_share_12500x1MiB_pinned_host_batch(ctx, oracle_lib):
+    import ctypes
+    from concurrent.futures import ThreadPoolExecutor
+    torch = _torch()
+    nobj, obj = 12500, MiB                                    # 100,000 / 8 GPUs
+    seed0 = SEED + 4
+    host = torch.empty(nobj * obj, dtype=torch.uint8, pin_memory=True)
+    base = host.data_ptr()
+    with ThreadPoolExecutor(_threads()) as ex:
+        list(ex.map(lambda j: oracle_lib.fill_splitmix_ptr(base + j * obj, 0, obj, seed0 + j), range(nobj)))
+    P = (ctypes.c_void_p * nobj)(*[base + j * obj for j in range(nobj)])
+    L = (ctypes.c_uint64 * nobj)(*([obj] * nobj))
+    out = ctypes.create_string_buffer(32 * nobj)
+    ctx._check(ctx._L.dm_root_batch(ctx._h, P, L, nobj, CHUNK, out), "dm_root_batch")
+    got = out.raw
+    with ThreadPoolExecutor(_threads()) as ex:
+        wants = list(ex.map(lambda j: oracle_lib.root_buffer_ptr(base + j * obj, obj, CHUNK)[1], range(nobj)))
+    bad = [j for j in range(nobj) if got[32 * j:32 * j + 32] != wants[j]]
+    assert not bad, f"{len(bad)} of {nobj} roots differ, first {bad[:5]}"
+
+
+def test_configs3_share_4096x32MiB_subtree(ctx, oracle_lib):
+    """Rank 5 of 8's share of the 1 TiB object: bytes [5 x 128 GiB, 6 x 128 GiB), 4,096 leaves.
+    12 levels reduce it to the one block root that rank contributes (2^12 leaves per block), which
+    is the merkletree root of those 4,096 leaves (a power of two: no odd-node duplication)."""
+    torch = _torch()
+    share, rank = 128 * GiB, 5
+    off = rank * share
+    seed = SEED + 3
+    _need_hbm(torch, share + 4 * GiB)
+    buf = torch.empty(share + 64, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(buf.data_ptr(), off, share, seed, s)
+    nodes = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    n = ctx.subtree_device_async(buf.data_ptr(), share, CHUNK, 12, nodes.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert n == 1
+    got = bytes(nodes[:32].cpu().numpy())
+    probe = bytes(buf[CHUNK - 64:CHUNK + 64].cpu().numpy())   # the generator at the share's offset
+    assert probe == oracle_lib.splitmix_bytes(128, seed, off=off + CHUNK - 64)
+    del buf
+    torch.cuda.empty_cache()
+    _, want = oracle_lib.root_synthetic(share, CHUNK, seed, nthreads=_threads(), base=off)
+    assert got == want
