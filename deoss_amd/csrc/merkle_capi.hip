@@ -745,7 +745,7 @@ int reduce_stages(dm_ctx* c, Dev& d, hipStream_t s, const uint8_t* in, uint64_t 
 // Leaf-kernel choice for a uniform-chunk object of n leaves: the more lanes a kernel spends per
 // leaf, the shorter each leaf's serial chain, as long as its workgroups fit the chip at once.
 // Returns DM_LEAF_WIDE, DM_LEAF_LATENCY, DM_LEAF_PAIR or DM_LEAF_QUAD.
-// Measured on MI355X (8 GiB object, profiles/r01_sweep_k1q4.log): K1Q wins up to 8,192 leaves
+// Measured on MI355X (8 GiB object, profiles/r01/LOGS.md#r01_sweep_k1q4.log): K1Q wins up to 8,192 leaves
 // (four 37 KiB-LDS workgroups per CU: 345.6 GiB/s at 8,192 leaves vs 274.7 for K1P), K1L up to
 // 16,384 (536 vs 397 for K1P, 223 for K1Q in two rounds of workgroups); past that one lane per
 // leaf with >= 2 waves per SIMD wins.  K1P stays selectable (DM_LEAF_PAIR).
@@ -1671,6 +1671,12 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
 }
 
 int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) { return ctx_create(out, devs, ndev, lanes); }
+
+int dm_keep_claimed(int hip_device, uint64_t* bytes) {
+    if (!bytes || hip_device < 0) return bad_arg();
+    *bytes = keep_claimed(hip_device);
+    return DM_OK;
+}
 
 void dm_destroy(dm_ctx* ctx) {
     if (!ctx) return;

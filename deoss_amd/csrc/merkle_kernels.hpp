@@ -657,7 +657,7 @@ static_assert(4 * kQuadLdsBytes <= (160u << 10), "four compact K1Q workgroups mu
 // addresses = 0 mod 8 runs the wide (<= 2 workgroups per CU) launch at 15.84 GiB/s (256 leaves)
 // and the compact (4 per CU) launch at 320 GiB/s (8,192 leaves); at 4 mod 8 the wide launch
 // drops to 12.85 and the compact one rises to 368 (reproducible over every odd and even shift,
-// profiles/r01f_align_ab.log).  So each step stream is pinned: 8-byte aligned, plus one 4-byte
+// profiles/r01/r01f_align_ab.log).  So each step stream is pinned: 8-byte aligned, plus one 4-byte
 // s_nop for the compact kernel (MIS).  Cause not isolated (instruction fetch / issue arbitration
 // between the two waves sharing a SIMD in the compact case).
 #define DM_QS_ALIGN ".p2align 3\n\t"
@@ -864,7 +864,7 @@ __global__ __launch_bounds__(kLatThreads) void leaf_kernel_quad(LeafArgs a) {
     } else {
         // The consumer carries the serial chains: give it issue priority over a producer or a
         // second consumer on its SIMD.  Measured on MI355X (tools/ab_builds.sh,
-        // profiles/r01g_prio_ab.log): 8,192 x 1 MiB leaves 367 -> 401 GiB/s, 256 x 32 MiB
+        // profiles/r01/LOGS.md#r01g_prio_ab.log): 8,192 x 1 MiB leaves 367 -> 401 GiB/s, 256 x 32 MiB
         // 15.82 -> 15.90, other K1Q shapes unchanged (priority 1 and 3 alike).
         __builtin_amdgcn_s_setprio(1);
         // lanes: leaf cq's e-quad = row lanes 4*(cq&1)+0..3, its a-quad 8 lanes higher (row_ror:8)

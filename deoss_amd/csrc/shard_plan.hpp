@@ -131,7 +131,7 @@ constexpr double kHostBytesPerS = 500e9;   // 2-socket DDR5 host (~1.2 TB/s peak
 // GPU (tools/shard_overhead.py, profiles/r03/LOGS.md#shard_overhead.log: +0.093 / 0.230 / 0.463 ms at
 // G = 2 / 4 / 8 over one device, i.e. ~0.06 ms per device), plus 0.1 ms for the all-gather of a
 // few KiB.  dm_exchange_timing measures that gather: 0.19 ms at G = 8 with virtual devices (the
-// D2D stand-in, profiles/r04/r04a_inproc.log); the RCCL gather over xGMI is recorded by the N = 8
+// D2D stand-in, profiles/r04/LOGS.md#r04a_inproc.log); the RCCL gather over xGMI is recorded by the N = 8
 // bench line (other_configs.in_process.sharded_object.exchange).  Sharding needs a >= 5 % gain, so
 // an error in this sub-millisecond term can only change the choice for calls under ~10 ms.
 inline double shard_overhead_ms(int G) { return G > 1 ? 0.10 + 0.06 * G : 0.0; }

@@ -26,7 +26,7 @@ import tempfile
 HERE = os.path.dirname(os.path.abspath(__file__))
 COUNTS = os.path.join(HERE, "isa_counts.json")
 # Issue slots per wave64 instruction relative to v_add_u32, measured on MI355X by
-# tools/valu_peak.hip (profiles/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
+# tools/valu_peak.hip (profiles/r01/r01_valu_peak.json): v_alignbit_b32 and v_add3_u32 run at half
 # the v_add_u32 / v_bitop3_b32 rate.
 SLOT_WEIGHTS = {"v_alignbit_b32": 2.0, "v_add3_u32": 2.0, "v_xad_u32": 2.0}
 # name: (symbol, (consumer lanes, producer lanes) per leaf-block)

@@ -62,6 +62,16 @@ class MerkleContext:
     def lane_count(self) -> int:
         return self._L.dm_lane_count(self._h)
 
+    @staticmethod
+    def keep_claimed(hip_device: int = 0) -> int:
+        """Idle lane-buffer bytes every live context of this process may keep on that GPU
+        (dm_keep_claimed): the per-GPU budget the default lane count is sized against."""
+        out = ctypes.c_uint64()
+        rc = load_library().dm_keep_claimed(hip_device, ctypes.byref(out))
+        if rc != 0:
+            raise DeossMerkleError(rc, "dm_keep_claimed failed")
+        return out.value
+
     def _check(self, rc: int, what: str) -> None:
         if rc == 0:
             return

@@ -67,8 +67,10 @@ enum {
  * shards it: a single object is then split by aligned chunk ranges across devices [0, G') and the
  * per-device subtree roots are gathered with RCCL ("C1"); a batch is split by
  * objects with no exchange.
- * Every GPU carries DEOSS_LANES call lanes (at most 8; unset: as many, up to 4, as keep at most half
- * of the first GPU's free HBM in idle lane buffers of <= 16 GiB each: 4 on an MI355X), each with its own streams,
+ * Every GPU carries DEOSS_LANES call lanes (at most 8; unset: 1 to 4, as many as keep at most half
+ * of the first GPU's free HBM in idle lane buffers of <= 16 GiB each AND, with every other live
+ * context's lanes on that GPU (dm_keep_claimed), at most half of its HBM: 4 for the first two
+ * default contexts on an MI355X, 1 after that), each with its own streams,
  * scratch and lock, so that many calls run on one GPU at once and concurrent callers (one gin
  * goroutine per upload) are not serialised behind each other's leaf chains.  A
  * lane's compute stream owns a hardware queue (created with a full CU mask); like every HIP stream
@@ -85,6 +87,10 @@ int dm_lane_count(dm_ctx *ctx);           /* call lanes per GPU */
 /* GPUs visible to this process (HIP device count; 0 without a usable GPU).  Lets a binding
  * default to every GPU of the node: dm_create(ctx, {0 .. dm_gpu_count()-1}, n). */
 int dm_gpu_count(void);
+/* Idle object-buffer bytes the live contexts of this process may keep on HIP device `hip_device`
+ * (sum over their lanes on it of the per-lane keep limit): the budget dm_create sizes its default
+ * lane count against.  0 on success. */
+int dm_keep_claimed(int hip_device, uint64_t *bytes);
 
 /* Page-locked host memory, visible to every GPU, for callers that want the zero-copy host paths.
  * dm_root_buffer / dm_root_chunks / dm_root_batch hash an object held in such memory in place: K1Q

@@ -3,8 +3,8 @@
 Round 4's N = 1 line grew to 28 KB and the driver could not parse it (BENCH_r04.json "parsed":
 null), so the headline went unmeasured.  bench.py now prints a compact line last (compact_line,
 at most LINE_MAX_BYTES) and writes the full record to a detail file.  These tests rebuild the
-compact line from the two full lines round 4 printed -- the N = 1 default run
-(profiles/r04/r04q_bench.log) and the 8-rank rehearsal (profiles/r04/r04m_rehearse8.log) -- and
+compact line from the two full lines round 4 printed -- the N = 1 default run and the 8-rank
+rehearsal (tests/golden/bench_lines_r04.json, from profiles/r04) -- and
 check its size and keys, that a failed extra or parity check turns `ok` false, and that a hung
 watchdogged leg ends the process with a non-zero status.
 """
@@ -13,8 +13,6 @@ import json
 import os
 import subprocess
 import sys
-
-import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -26,12 +24,10 @@ REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 
 def _full_line(name):
-    path = os.path.join(ROOT, "profiles", "r04", name)
-    if not os.path.exists(path):
-        pytest.skip(f"{path} absent")
-    with open(path) as f:
-        lines = [x for x in f.read().splitlines() if x.startswith("{")]
-    return json.loads(lines[-1])
+    """Round 4's full lines, kept in tests/golden/bench_lines_r04.json (from profiles/r04)."""
+    with open(os.path.join(ROOT, "tests", "golden", "bench_lines_r04.json")) as f:
+        d = json.load(f)
+    return d[{"r04q_bench.log": "n1", "r04m_rehearse8.log": "n8"}[name]]
 
 
 def _size(line):

@@ -2,7 +2,7 @@
 object out of libdeoss_merkle.so and disassembles it).
 
 Every K1Q step instruction is 8 bytes, and on MI355X where the stream sits mod 8 changed the rate
-by 15-19 % (profiles/r01f_align_ab.log): the wide kernel (<= 2 workgroups per
+by 15-19 % (profiles/r01/r01f_align_ab.log): the wide kernel (<= 2 workgroups per
 CU, the headline) must run at 0 mod 8, the compact kernel (4 per CU) at 4 mod 8.  The kernels
 pin this with `.p2align 3` (+ one s_nop for the compact one); this test keeps a later edit from
 silently undoing it.

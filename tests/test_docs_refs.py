@@ -1,6 +1,6 @@
 """CPU guards on the evidence the docs cite: every `profiles/...` path named in DESIGN.md,
 INTEGRATION.md and README.md exists, every `profiles/rNN/LOGS.md#name` anchor is a section of that
-file, every bare `r04x_*.log` DESIGN.md names is in profiles/r04/, and profiles/extras_traffic.json
+file, every bare `rNNx_*.log` the docs name is in profiles/rNN/ (or its LOGS.md), and profiles/extras_traffic.json
 (read by bench.py for the extras' roofline traffic) covers every extra bench.py reports."""
 import json
 import os
@@ -38,10 +38,18 @@ def test_logs_anchors_exist():
     assert not bad, bad
 
 
-def test_round4_logs_named_in_design_exist():
-    names = set(re.findall(r"`(r04[a-z]+_[A-Za-z0-9_\-]+\.log)`", _read("DESIGN.md")))
-    assert names
-    missing = [n for n in names if not os.path.exists(os.path.join(ROOT, "profiles", "r04", n))]
+def test_round_logs_named_in_docs_exist():
+    """A bare `rNNx_name.log` in the docs is a file of profiles/rNN/ or a section of its LOGS.md."""
+    missing = []
+    for doc in DOCS:
+        for name, rnd in set(re.findall(r"`((r0\d)[a-z]*_[A-Za-z0-9_\-]+\.log)`", _read(doc))):
+            d = os.path.join(ROOT, "profiles", rnd)
+            logs = os.path.join(d, "LOGS.md")
+            if os.path.exists(os.path.join(d, name)):
+                continue
+            if os.path.exists(logs) and f"## {name}" in _read(os.path.relpath(logs, ROOT)):
+                continue
+            missing.append((doc, name))
     assert not missing, missing
 
 

@@ -75,17 +75,53 @@ def test_lane_growth_near_full_hbm_waits_for_deferred_frees(oracle_lib):
 
 def test_last_call_devices_and_lane_default(oracle_lib):
     """dm_last_call_devices: nothing before the first call, then the one GPU a whole call ran on;
-    the lane default sizes from free HBM (4 on an MI355X: 4 x 16 GiB kept buffers <= half of it)."""
+    the lane default is sized per GPU: within half the free HBM and, together with
+    every live context's claim (dm_keep_claimed), within half of the GPU's HBM."""
     from deoss_amd import MerkleContext
+    from test_gpu_parity import expected_default_lanes
     if "DEOSS_LANES" in os.environ:
         pytest.skip("DEOSS_LANES set")
+    torch = _torch()
+    want = expected_default_lanes(torch)
+    before = MerkleContext.keep_claimed(0)
     with MerkleContext() as c:
+        assert c.lane_count == want
+        assert MerkleContext.keep_claimed(0) == before + want * (16 << 30)
         assert c.last_call_devices() == ([], [], -1)
         data = oracle_lib.splitmix_bytes(3 << 20, 5)
         assert c.root_buffer(data, 1 << 16, want_leaves=False)[1] == oracle_lib.root_buffer(data, 1 << 16)[1]
         devs, ids, lane = c.last_call_devices()
         assert devs == [0] and ids == [0] and 0 <= lane < c.lane_count
-        assert c.lane_count == 4
+    assert MerkleContext.keep_claimed(0) == before
+
+
+def test_lane_budget_is_per_gpu():
+    """default contexts share one keep budget per GPU.  Contexts opened together get
+    4, 4, ... lanes until their claims reach half the GPU's HBM, then 1 each; closing one returns
+    its claim."""
+    from deoss_amd import MerkleContext
+    from test_gpu_parity import expected_default_lanes
+    if "DEOSS_LANES" in os.environ:
+        pytest.skip("DEOSS_LANES set")
+    torch = _torch()
+    _, total = torch.cuda.mem_get_info()
+    base = MerkleContext.keep_claimed(0)          # contexts the session already holds
+    held = []
+    try:
+        for _ in range(5):
+            want = expected_default_lanes(torch)
+            held.append(MerkleContext())
+            assert held[-1].lane_count == want
+        claimed = MerkleContext.keep_claimed(0)
+        assert claimed == base + sum(c.lane_count for c in held) * (16 << 30)
+        assert claimed >= total // 2                         # 5 default contexts reach half of 288 GB
+        assert held[-1].lane_count == 1                      # ... so the last one gets a single lane
+        last = held.pop()
+        last.close()
+        assert MerkleContext.keep_claimed(0) == claimed - (16 << 30)
+    finally:
+        for c in held:
+            c.close()
 
 
 @pytest.mark.parametrize("G", [2, 8])
