@@ -111,12 +111,16 @@ AllocLocks& alloc_locks() {
 std::mutex& dev_mutex(int dev) { return alloc_locks().dev[(unsigned)dev % AllocLocks::kDevs]; }
 
 // hipMalloc(n) on device `dev` (current on the calling thread), or hipErrorOutOfMemory without
-// calling hipMalloc when less than n + kMallocHeadroom is free.
+// calling hipMalloc when less than n + kMallocHeadroom is free.  DM_ALLOC_PRECHECK=0 builds an A/B
+// variant without the free-memory check (the lock alone), never the shipped library.
+#ifndef DM_ALLOC_PRECHECK
+#define DM_ALLOC_PRECHECK 1
+#endif
 hipError_t dev_alloc(int dev, void** p, size_t n) {
     *p = nullptr;
     std::lock_guard<std::mutex> lk(dev_mutex(dev));
     size_t fr = 0, tot = 0;
-    if (free_on(dev, &fr, &tot) && fr < n + kMallocHeadroom) return hipErrorOutOfMemory;
+    if (DM_ALLOC_PRECHECK && free_on(dev, &fr, &tot) && fr < n + kMallocHeadroom) return hipErrorOutOfMemory;
     hipError_t e = hipMalloc(p, n);
     if (e != hipSuccess) {
         (void)hipGetLastError();
