@@ -262,8 +262,10 @@ def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, 
     """N > 1: BASELINE configs[1]'s one 8 GiB object sharded over all N ranks (total work fixed),
     beside the weak-scaling headline.  At 32 MiB chunks the object is 256 leaves: one GPU already
     runs all 256 serial chains at once (0.49 s each), so splitting them over N GPUs cannot shorten
-    the step -- strong scaling is ~1x by construction; this measures it.  Checked:
-    the sharded root against the single-GPU root and the CPU restatement of the same bytes."""
+    the step -- strong scaling is ~1x by construction; this measures it:
+    speedup_vs_one_gpu = the same object's root on rank 0's GPU alone (single_gpu_ms, timed in the
+    parity leg) / the sharded step.  Checked: the sharded root against that single-GPU root and the
+    CPU restatement of the same bytes."""
     import copy
     ns = copy.copy(args)
     ns.total_gib, ns.steps, ns.warmup, ns.no_extras = 8.0, 3, 1, True
@@ -275,7 +277,9 @@ def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, 
     par = r.get("parity") or {}
     res = {"workload": "configs[1] strong: one 8 GiB object (256 leaves of 32 MiB) over "
                        f"{world} GPUs", "value": r["value"], "unit": "GiB/s", "ms_per_step": r["ms_per_step"],
-           "steps": ns.steps, "bit_exact": par.get("bit_exact"),
+           "steps": ns.steps, "bit_exact": par.get("bit_exact"), "single_gpu_ms": par.get("single_gpu_ms"),
+           "speedup_vs_one_gpu": (round(par["single_gpu_ms"] / r["ms_per_step"], 3)
+                                  if par.get("single_gpu_ms") and r.get("ms_per_step") else None),
            "speedup_vs_one_gpu_share_of_weak": round(r["value"] / weak_per_gpu, 3) if weak_per_gpu else None,
            "note": "~1x by construction at 32 MiB chunks: 256 chains of ~0.49 s run concurrently on one GPU already",
            "wall_s": round(time.perf_counter() - t0, 2)}
@@ -835,6 +839,11 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
         ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
         torch.cuda.synchronize()
         single = bytes(one.cpu().numpy()).hex()
+        if prefix == total:   # the whole object on this one GPU, timed once more (warm): the strong leg's 1-GPU time
+            t0 = time.perf_counter()
+            ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
+            torch.cuda.synchronize()
+            res["single_gpu_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
         del full
         torch.cuda.empty_cache()
         res.update({"prefix_bytes": prefix, "prefix_sharded_root": sharded_prefix, "prefix_single_gpu_root": single,

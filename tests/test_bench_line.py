@@ -63,12 +63,13 @@ def test_compact_line_n8_rehearsal():
     full = _full_line("r04m_rehearse8.log")
     full = copy.deepcopy(full)
     full["strong_scaling"] = {"workload": "configs[1] strong", "value": 16.3, "unit": "GiB/s", "bit_exact": True,
-                              "speedup_vs_one_gpu_share_of_weak": 1.0}
+                              "single_gpu_ms": 490.0, "speedup_vs_one_gpu": 1.0, "speedup_vs_one_gpu_share_of_weak": 1.0}
     line = bench.compact_line(full, None)
     assert _size(line) <= bench.LINE_MAX_BYTES
     for k in REQUIRED + ("parity", "launch", "extras", "strong_scaling"):
         assert k in line, k
     assert line["launch"]["world_size"] == full["launch"]["world_size"]
+    assert line["strong_scaling"]["speedup_vs_one_gpu"] == 1.0
     assert set(line["extras"]) == {"configs[3]", "configs[4]", "in_process"}
     ip = line["extras"]["in_process"]
     assert ip["bit_exact"] is True and ip["sharded_object"]["bit_exact"] is True
