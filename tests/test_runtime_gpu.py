@@ -173,3 +173,38 @@ def test_rs_create_does_not_wait_for_lane_chains(oracle_lib):
         shards = [oracle_lib.splitmix_bytes(4096, 40 + j) for j in range(4)]
         assert enc.Encode(shards + [bytes(4096)] * 8)[4:] == oracle_lib.rs_encode(shards, 8)
         enc.close()
+
+
+def test_context_churn_returns_memory_and_claims(oracle_lib):
+    """A long-lived gateway opens and closes contexts and streams: 40 rounds of create -> a
+    pageable-buffer root (grows the lane's object buffer), a pinned zero-copy root, a streamed
+    upload -> destroy, every result checked.  Afterwards the device's free memory is back within
+    256 MiB of where it started (every hipMalloc of the library is matched by a hipFree through
+    the one allocator) and the per-GPU keep claims are back to the session's."""
+    import numpy as np
+    torch = _torch()
+    from deoss_amd import MerkleContext, PinnedBuffer
+    data = oracle_lib.splitmix_bytes((48 << 20) + 123, 0xC0FFEE)
+    _, want = oracle_lib.root_buffer(data, 1 << 20, nthreads=8)
+    pin = PinnedBuffer(len(data))
+    pin.array()[:] = np.frombuffer(data, dtype=np.uint8)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0, _ = torch.cuda.mem_get_info()
+    claim0 = MerkleContext.keep_claimed(0)
+    try:
+        for i in range(40):
+            with MerkleContext(lanes=2) as c:
+                assert c.root_buffer(data, 1 << 20, want_leaves=False)[1] == want
+                assert c.root_buffer_ptr(pin.ptr, len(data), 1 << 20)[1] == want
+                if i % 4 == 0:
+                    s = c.open_stream(1 << 20)
+                    for o in range(0, len(data), 5 << 20):
+                        s.write(data[o:o + (5 << 20)])
+                    assert s.close()[1] == want
+        torch.cuda.synchronize()
+        free1, _ = torch.cuda.mem_get_info()
+        assert abs(free0 - free1) <= (256 << 20), (free0, free1)
+        assert MerkleContext.keep_claimed(0) == claim0
+    finally:
+        pin.free()
