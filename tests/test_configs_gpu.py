@@ -10,6 +10,8 @@ bench.py).  The oracle is the checker only; every result comes from libdeoss_mer
               HBM at the share's byte offset, reduced 12 levels by dm_subtree_device_async (the
               block root that rank sends in the RCCL all-gather), against the oracle's root of
               the same leaf range regenerated leaf by leaf (or_root_synthetic_at).
+  configs[1]  the 8 GiB object made ragged at full size (257 / 256 / 255 leaves with short last
+              leaves): merkletree's odd-count duplication at the headline's scale, leaves and root.
 
 Reference path: /root/reference/common/hashtree/types.go:19-39 (NewHashTree: one merkletree per
 object, types.go:38), hashtree.go:23-30 (leaf = SHA-256 of the chunk)."""
@@ -123,3 +125,29 @@ def test_configs3_share_4096x32MiB_subtree(ctx, oracle_lib):
     torch.cuda.empty_cache()
     _, want = oracle_lib.root_synthetic(share, CHUNK, seed, nthreads=_threads(), base=off)
     assert got == want
+
+
+@pytest.mark.parametrize("length", [8 * GiB + 8, 8 * GiB - 8, 8 * GiB - CHUNK + 4096])
+def test_configs1_ragged_full_size(ctx, oracle_lib, length):
+    """configs[1]'s 8 GiB object, made ragged at full size: 257 leaves whose last is one 8-byte
+    block (the odd leaf duplicated at level 0, then a lone node self-paired up 8 levels), 256
+    leaves whose last is 8 bytes short (multi-block leaf ending inside a block), and 255 leaves
+    with a 4 KiB last leaf (odd counts at several levels).  Device-generated bytes; the oracle
+    regenerates them leaf by leaf (or_root_synthetic); leaf digests checked too."""
+    torch = _torch()
+    seed = SEED + 1
+    _need_hbm(torch, length + 4 * GiB)
+    buf = torch.empty(length + 64, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ctx.fill_synthetic_async(buf.data_ptr(), 0, length, seed, s)
+    n = (length + CHUNK - 1) // CHUNK
+    root = torch.zeros(32, dtype=torch.uint8, device="cuda")
+    lv = torch.zeros(32 * n, dtype=torch.uint8, device="cuda")
+    ctx.root_device_async(buf.data_ptr(), length, CHUNK, root.data_ptr(), lv.data_ptr(), s)
+    torch.cuda.synchronize()
+    got, got_leaves = bytes(root.cpu().numpy()), bytes(lv.cpu().numpy())
+    del buf
+    torch.cuda.empty_cache()
+    leaves, want = oracle_lib.root_synthetic(length, CHUNK, seed, nthreads=_threads(), want_leaves=True)
+    assert got_leaves == leaves
+    assert got == want, (length, got.hex(), want.hex())

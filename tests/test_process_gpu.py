@@ -771,3 +771,57 @@ def test_skip_segment_files(ctx, oracle_lib, tmp_path, monkeypatch):
     assert st.close()[1] == want_fid.hex()
     assert set(os.listdir(tmp_path / "b")) == frag_names
     p.close()
+
+
+def test_process_device_bench_scale_cross_paths(ctx, oracle_lib):
+    """FullProcessing at the bench workload's scale (`bench.py --workload process`: 8 GiB in HBM =
+    256 segments -> 3,328 names + fid), every output cross-checked against independent GPU paths
+    (size-independent properties): segment names and fid == the uniform-chunk Merkle tree of the
+    object at 32 MiB (K1Q, the headline path); data-fragment names == its leaves at 8 MiB; parity ==
+    a standalone rs encode of the object; parity names == the leaves of that parity at 8 MiB.
+    Segments 0 and 255 are also checked against the CPU restatement."""
+    torch = _torch()
+    p = _processor(ctx)
+    seg, k, m = 32 << 20, 4, 8
+    frag = seg // k
+    nseg = 256
+    nbytes = nseg * seg
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    assert torch.cuda.mem_get_info()[0] >= 5 * nbytes + (4 << 30)
+    obj = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    p.ctx.fill_synthetic_async(obj.data_ptr(), 0, nbytes, 0xDE0559)
+    parity = torch.empty(nseg * m * frag, dtype=torch.uint8, device="cuda")
+    segh = torch.empty(nseg * 32, dtype=torch.uint8, device="cuda")
+    fragh = torch.empty(nseg * (k + m) * 32, dtype=torch.uint8, device="cuda")
+    fid = torch.empty(32, dtype=torch.uint8, device="cuda")
+    p.process_device_async(obj.data_ptr(), nbytes, parity.data_ptr(), segh.data_ptr(), fragh.data_ptr(),
+                           fid.data_ptr())
+    torch.cuda.synchronize()
+    fh = fragh.view(nseg, k + m, 32)
+
+    def tree(ptr, length, chunk):
+        n = length // chunk
+        r = torch.zeros(32, dtype=torch.uint8, device="cuda")
+        lv = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        p.ctx.root_device_async(ptr, length, chunk, r.data_ptr(), lv.data_ptr(), 0)
+        torch.cuda.synchronize()
+        return r, lv.view(n, 32)
+
+    r32, l32 = tree(obj.data_ptr(), nbytes, seg)
+    assert torch.equal(l32, segh.view(nseg, 32)) and torch.equal(r32, fid)
+    _, l8 = tree(obj.data_ptr(), nbytes, frag)
+    assert torch.equal(l8.view(nseg, k, 32), fh[:, :k])
+    par2 = torch.empty_like(parity)
+    p.enc.encode_device_async(obj.data_ptr(), seg, par2.data_ptr(), m * frag, frag, nseg, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(par2, parity)
+    del par2
+    _, lp = tree(parity.data_ptr(), nseg * m * frag, frag)
+    assert torch.equal(lp.view(nseg, m, 32), fh[:, k:])
+    for s in (0, nseg - 1):
+        host = obj[s * seg:(s + 1) * seg].cpu().numpy().tobytes()
+        want_seg, want_frag, _, _ = oracle_lib.full_processing(host, seg, k, m, nthreads=8)
+        assert segh[s * 32:(s + 1) * 32].cpu().numpy().tobytes() == want_seg
+        assert fh[s].cpu().numpy().tobytes() == want_frag
+    p.close()

@@ -172,3 +172,47 @@ def test_device_argument_errors(rs48):
         rs48.encode_device_async(t.data_ptr() + 1, 0, t.data_ptr(), 0, 16, 1, 0)
     with pytest.raises(DeossMerkleError):
         rs48.encode_device_async(t.data_ptr(), 0, t.data_ptr(), 0, 24, 1, 0)
+
+
+def test_bench_scale_linearity_and_round_trip(rs48, oracle_lib):
+    """The bench workload's scale (256 segments of 32 MiB = 8 GiB of data -> 16 GiB of parity,
+    `bench.py --workload rs`), checked by size-independent properties on the device: the code is
+    linear over GF(2^8) -- parity(A ^ B) == parity(A) ^ parity(B) for every byte of all 256
+    segments -- first and last segments' parity equal the oracle's, and 16 segments spread over
+    the object survive an 8-fragment erasure and device reconstruction bit-exact."""
+    torch = _torch()
+    shard, nseg = 8 << 20, 256
+    seg = 4 * shard
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    assert free >= 9 * nseg * seg + (4 << 30), free               # 3 objects (8 GiB) + 3 parity sets (16 GiB)
+    ctx = rs48._ctx
+    a = torch.empty(nseg * seg, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    ctx.fill_synthetic_async(a.data_ptr(), 0, nseg * seg, 0xDE0557, 0)
+    ctx.fill_synthetic_async(b.data_ptr(), 0, nseg * seg, 0xDE0558, 0)
+    c = torch.bitwise_xor(a, b)
+    pa, pb, pc = (torch.empty(nseg * 2 * seg, dtype=torch.uint8, device="cuda") for _ in range(3))
+    for d, p in ((a, pa), (b, pb), (c, pc)):
+        rs48.encode_device_async(d.data_ptr(), seg, p.data_ptr(), 2 * seg, shard, nseg, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.bitwise_xor(pa, pb), pc)               # linearity, all 16 GiB of parity
+    del b, c, pb, pc
+    torch.cuda.empty_cache()
+    for s in (0, nseg - 1):
+        host = a[s * seg:(s + 1) * seg].cpu().numpy()
+        want = oracle_lib.rs_encode([host[j * shard:(j + 1) * shard].tobytes() for j in range(4)], 8, nthreads=8)
+        got = pa[s * 2 * seg:(s + 1) * 2 * seg].cpu().numpy()
+        assert [got[i * shard:(i + 1) * shard].tobytes() for i in range(8)] == want, s
+    rnd = random.Random(5)
+    for s in range(0, nseg, nseg // 16):
+        frags = torch.cat([a[s * seg:(s + 1) * seg], pa[s * 2 * seg:(s + 1) * 2 * seg]]).view(12, shard)
+        keep = frags.clone()
+        lost = sorted(rnd.sample(range(12), 8))
+        for i in lost:
+            frags[i].fill_(0x5A)
+        rs48.reconstruct_device_async([frags[i].data_ptr() for i in range(12)], [i not in lost for i in range(12)],
+                                      shard, 0)
+        torch.cuda.synchronize()
+        assert torch.equal(frags, keep), (s, lost)
