@@ -1574,6 +1574,9 @@ namespace {
 // process context and any other dm_ctx on the same GPU share one budget.
 std::mutex g_keep_mu;
 std::map<int, uint64_t> g_keep_claimed;
+// dm_create / dm_create_lanes hold this from sizing the lanes to claiming them, so two contexts
+// created at once never both size themselves against the same unclaimed budget.
+std::mutex g_create_mu;
 
 uint64_t keep_claimed(int dev) {
     std::lock_guard<std::mutex> lk(g_keep_mu);
@@ -1588,7 +1591,7 @@ void keep_claim(int dev, int64_t delta) {
 }
 
 // Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else sized from the
-// first GPU's HBM.  Every lane runs on a hardware queue of its own (init_device), so L lanes
+// context's first GPU's HBM and claims (a multi-GPU context uses the same count on every GPU).  Every lane runs on a hardware queue of its own (init_device), so L lanes
 // overlap L large calls (measured: 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound
 // at 4 for pinned 8 GiB ones; tools/lanes_probe.py, profiles/r03/LOGS.md#r03w_lanes.log).  What a lane
 // costs while idle is the object buffer it keeps between calls, at most kLaneKeepBytes (16 GiB),
@@ -1671,10 +1674,14 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     DeviceRestore dr;
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return set_err(DM_ERR_NODEV, "no usable GPU");
     if (first < 0 || first >= count) return bad_arg();
+    std::lock_guard<std::mutex> lk(g_create_mu);
     return ctx_create(out, devs, ndev, default_lanes(first));
 }
 
-int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) { return ctx_create(out, devs, ndev, lanes); }
+int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) {
+    std::lock_guard<std::mutex> lk(g_create_mu);
+    return ctx_create(out, devs, ndev, lanes);
+}
 
 int dm_keep_claimed(int hip_device, uint64_t* bytes) {
     if (!bytes || hip_device < 0) return bad_arg();
