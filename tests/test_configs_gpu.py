@@ -4,8 +4,9 @@ bench.py).  The oracle is the checker only; every result comes from libdeoss_mer
 
   configs[2]  4,096 x 4 MiB objects resident in HBM, one root each (dm_root_batch_device_async):
               many independent trees of one 4 MiB leaf (chunk 32 MiB), root = SHA256(h || h).
-  configs[4]  one GPU's share of 100,000 x 1 MiB host objects: 12,500 x 1 MiB in pinned host
-              memory through dm_root_batch (the upload regime: host buffers in, roots out).
+  configs[4]  one GPU's share of 100,000 x 1 MiB host objects: 12,500 x 1 MiB in pinned and in
+              pageable host memory through dm_root_batch (the upload regime: host buffers in,
+              roots out).
   configs[3]  one GPU's share of the 1 TiB object: 4,096 x 32 MiB leaves (128 GiB) generated in
               HBM at the share's byte offset, reduced 12 levels by dm_subtree_device_async (the
               block root that rank sends in the RCCL all-gather), against the oracle's root of
@@ -81,13 +82,16 @@ def test_configs2_4096x4MiB_device_batch(ctx, oracle_lib):
     assert got[:32] == hashlib.sha256(leaf + leaf).digest()
 
 
-def test_configs4_share_12500x1MiB_pinned_host_batch(ctx, oracle_lib):
+@pytest.mark.parametrize("pinned", [True, False])
+def test_configs4_share_12500x1MiB_host_batch(ctx, oracle_lib, pinned):
+    """Pinned bodies are read in place by K1Q over PCIe (zero-copy); pageable ones stream through
+    the pinned ring with H2D copies overlapped with hashing (configs[4]'s "overlapped H2D")."""
     import ctypes
     from concurrent.futures import ThreadPoolExecutor
     torch = _torch()
     nobj, obj = 12500, MiB                                    # 100,000 / 8 GPUs
     seed0 = SEED + 4
-    host = torch.empty(nobj * obj, dtype=torch.uint8, pin_memory=True)
+    host = torch.empty(nobj * obj, dtype=torch.uint8, pin_memory=pinned)
     base = host.data_ptr()
     with ThreadPoolExecutor(_threads()) as ex:
         list(ex.map(lambda j: oracle_lib.fill_splitmix_ptr(base + j * obj, 0, obj, seed0 + j), range(nobj)))
