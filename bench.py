@@ -205,6 +205,9 @@ def main() -> None:
         progress("strong-scaling leg: configs[1]'s 8 GiB object over every rank")
         out["strong_scaling"] = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier,
                                                    out["value"] / world)
+        progress("strong-scaling leg at 4 KiB chunks (2,097,152 leaves)")
+        out["strong_scaling_4KiB"] = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo,
+                                                        barrier, out["value"] / world, chunk=4096)
     if world == 1 and rank == 0 and not args.no_extras:
         out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
         progress("latency block")
@@ -258,31 +261,39 @@ def watchdog_check(args) -> None:
     emit(out, args.detail_out)
 
 
-def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu):
+def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu,
+                       chunk=32 << 20):
     """N > 1: BASELINE configs[1]'s one 8 GiB object sharded over all N ranks (total work fixed),
-    beside the weak-scaling headline.  At 32 MiB chunks the object is 256 leaves: one GPU already
-    runs all 256 serial chains at once (0.49 s each), so splitting them over N GPUs cannot shorten
-    the step -- strong scaling is ~1x by construction; this measures it:
-    speedup_vs_one_gpu = the same object's root on rank 0's GPU alone (single_gpu_ms, timed in the
-    parity leg) / the sharded step.  Checked: the sharded root against that single-GPU root and the
-    CPU restatement of the same bytes."""
+    beside the weak-scaling headline; speedup_vs_one_gpu = the same object's root on rank 0's GPU
+    alone (single_gpu_ms, timed in the parity leg) / the sharded step.  Checked: the sharded root
+    against that single-GPU root and the CPU restatement of the same bytes.
+      chunk 32 MiB (configs[1]'s): 256 leaves -- one GPU already runs all 256 serial chains at once
+        (0.49 s each), so splitting them over N GPUs cannot shorten the step: ~1x by construction
+        (DESIGN.md §7);
+      chunk 4 KiB (the sweep's smallest): 2,097,152 leaves -- one GPU is VALU-throughput-bound (K1,
+        ~1.5 TB/s), so N GPUs split the work: the regime where north_star's "6x at 8 GPUs" can hold."""
     import copy
     ns = copy.copy(args)
-    ns.total_gib, ns.steps, ns.warmup, ns.no_extras = 8.0, 3, 1, True
+    ns.total_gib, ns.chunk, ns.no_extras = 8.0, chunk, True
+    ns.steps, ns.warmup = (3, 1) if chunk >= (1 << 20) else (20, 3)   # 0.49 s vs ~1-6 ms steps
     t0 = time.perf_counter()
     try:
         r = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
     except Exception as e:   # reported, never fatal to the headline line
         return {"error": f"{type(e).__name__}: {e}"}
     par = r.get("parity") or {}
-    res = {"workload": "configs[1] strong: one 8 GiB object (256 leaves of 32 MiB) over "
-                       f"{world} GPUs", "value": r["value"], "unit": "GiB/s", "ms_per_step": r["ms_per_step"],
+    n = (8 << 30) // chunk
+    res = {"workload": f"configs[1] strong: one 8 GiB object ({n} leaves of {chunk} B) over {world} GPUs",
+           "chunk": chunk, "value": r["value"], "unit": "GiB/s", "ms_per_step": r["ms_per_step"],
            "steps": ns.steps, "bit_exact": par.get("bit_exact"), "single_gpu_ms": par.get("single_gpu_ms"),
            "speedup_vs_one_gpu": (round(par["single_gpu_ms"] / r["ms_per_step"], 3)
                                   if par.get("single_gpu_ms") and r.get("ms_per_step") else None),
-           "speedup_vs_one_gpu_share_of_weak": round(r["value"] / weak_per_gpu, 3) if weak_per_gpu else None,
-           "note": "~1x by construction at 32 MiB chunks: 256 chains of ~0.49 s run concurrently on one GPU already",
            "wall_s": round(time.perf_counter() - t0, 2)}
+    if chunk >= (1 << 20):
+        res["speedup_vs_one_gpu_share_of_weak"] = round(r["value"] / weak_per_gpu, 3) if weak_per_gpu else None
+        res["note"] = "~1x by construction at 32 MiB chunks: 256 chains of ~0.49 s run concurrently on one GPU already"
+    else:
+        res["note"] = "throughput regime: 2,097,152 leaves split over the GPUs (K1 per rank)"
     return res
 
 
@@ -710,11 +721,12 @@ def compact_line(out, detail_path=None):
     for k in ("same_device", "note", "ranks"):
         if k in out:
             line[k] = out[k]
-    st = out.get("strong_scaling")
-    if isinstance(st, dict):
-        line["strong_scaling"] = st
-        if st.get("bit_exact") is False or "error" in st:
-            problems.append("strong_scaling")
+    for key in ("strong_scaling", "strong_scaling_4KiB"):
+        st = out.get(key)
+        if isinstance(st, dict):
+            line[key] = {k: v for k, v in st.items() if k != "note"}
+            if st.get("bit_exact") is False or "error" in st:
+                problems.append(key)
     extras = {}
     for name, r in (out.get("other_configs") or {}).items():
         extras[name] = _in_process_line(r) if name == "in_process" else _extra_line(r)
@@ -837,11 +849,13 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
         ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
         torch.cuda.synchronize()
         single = bytes(one.cpu().numpy()).hex()
-        if prefix == total:   # the whole object on this one GPU, timed once more (warm): the strong leg's 1-GPU time
+        if prefix == total:   # the whole object on this one GPU, timed warm: the strong leg's 1-GPU time
+            reps = 3 if chunk >= (1 << 20) else 10
             t0 = time.perf_counter()
-            ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
+            for _ in range(reps):
+                ctx.root_device_async(full.data_ptr(), prefix, chunk, one.data_ptr(), 0, sptr)
             torch.cuda.synchronize()
-            res["single_gpu_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
+            res["single_gpu_ms"] = round((time.perf_counter() - t0) * 1e3 / reps, 3)
         del full
         torch.cuda.empty_cache()
         res.update({"prefix_bytes": prefix, "prefix_sharded_root": sharded_prefix, "prefix_single_gpu_root": single,

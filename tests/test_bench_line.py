@@ -64,8 +64,13 @@ def test_compact_line_n8_rehearsal():
     full = copy.deepcopy(full)
     full["strong_scaling"] = {"workload": "configs[1] strong", "value": 16.3, "unit": "GiB/s", "bit_exact": True,
                               "single_gpu_ms": 490.0, "speedup_vs_one_gpu": 1.0, "speedup_vs_one_gpu_share_of_weak": 1.0}
+    full["strong_scaling_4KiB"] = {"workload": "configs[1] strong: one 8 GiB object (2097152 leaves of 4096 B) over "
+                                   "8 GPUs", "chunk": 4096, "value": 5000.0, "unit": "GiB/s", "ms_per_step": 1.6,
+                                   "bit_exact": True, "single_gpu_ms": 5.6, "speedup_vs_one_gpu": 3.5,
+                                   "note": "throughput regime"}
     line = bench.compact_line(full, None)
     assert _size(line) <= bench.LINE_MAX_BYTES
+    assert line["strong_scaling_4KiB"]["speedup_vs_one_gpu"] == 3.5 and "note" not in line["strong_scaling_4KiB"]
     for k in REQUIRED + ("parity", "launch", "extras", "strong_scaling"):
         assert k in line, k
     assert line["launch"]["world_size"] == full["launch"]["world_size"]
