@@ -23,12 +23,13 @@ import sys
 import time
 
 # Shared helpers and the workloads measured beside the headline; tests and tools reach some of
-# them as bench.<name>.
-from bench_common import (
+# them as bench.<name> (re-exports: _pcts, PCIE_PEAK_GBS, EXTRA_ROOF, extras_traffic, extra_roofline,
+# cpu_fp_baseline, cpu_root_baseline).
+from bench_common import (  # noqa: F401
     ROOT, HBM_PEAK_GBS, VALU_SLOT_PEAK, MAX_CLOCK_HZ, ISSUE_CYCLES_ONE_WAVE, SEED, progress,
     start_heartbeat, env_int, host_cpu_facts, cpu_share, PIN_MERKLE, pinning_for, blocks_for, _pcts,
     PCIE_PEAK_GBS)
-from bench_workloads import (
+from bench_workloads import (  # noqa: F401
     latency_block, in_process_configs, _summary, EXTRA_ROOF, extras_traffic, extra_roofline, driver_extras,
     cpu_fp_baseline, cpu_root_baseline, run_files, run_plumbing, run_upload, run_rs, run_process,
     run_fullprocessing, run_process_upload, run_proofs, run_concurrent, run_batch)
