@@ -725,7 +725,7 @@ def compact_line(out, detail_path=None):
     for key in ("strong_scaling", "strong_scaling_4KiB"):
         st = out.get(key)
         if isinstance(st, dict):
-            line[key] = {k: v for k, v in st.items() if k != "note"}
+            line[key] = {k: _short(v, 160) for k, v in st.items() if k != "note"}
             if st.get("bit_exact") is False or "error" in st:
                 problems.append(key)
     extras = {}

@@ -125,3 +125,20 @@ def test_watchdog_hang_exits_nonzero(tmp_path):
     assert line["ok"] is False and line["problems"] == ["in_process"]
     assert "watchdog" in line["extras"]["in_process"]["error"]
     assert os.path.exists(tmp_path / "d.json")
+
+
+def test_strong_leg_error_and_missing_blocks():
+    """A strong leg that raised shows as an error and turns ok false; a line without roofline,
+    CPU baseline or extras (a bare N > 1 run with --no-extras) still fits and carries the contract keys."""
+    full = copy.deepcopy(_full_line("r04m_rehearse8.log"))
+    full["strong_scaling_4KiB"] = {"error": "RuntimeError: " + "y" * 3000}
+    line = bench.compact_line(full, None)
+    assert line["ok"] is False and "strong_scaling_4KiB" in line["problems"]
+    assert _size(line) <= bench.LINE_MAX_BYTES and len(line["strong_scaling_4KiB"]["error"]) <= 160
+    bare = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    line = bench.compact_line(bare, None)
+    assert line["ok"] is True and _size(line) < 1500
+    for k in REQUIRED:
+        if k != "roofline":
+            assert k in line, k

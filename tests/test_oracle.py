@@ -163,6 +163,23 @@ def test_root_synthetic_matches_buffer(oracle_lib):
         oracle_lib.root_synthetic(64, 100, 1)
 
 
+def test_root_synthetic_at_offset_matches_buffer(oracle_lib):
+    """or_root_synthetic_at: one GPU's share of a larger object (bytes [base, base + len) of the
+    stream) -- the configs[3] share checker -- equals the buffer root of those same bytes, and the
+    leaves of the shares of an object are the whole object's leaves, in order."""
+    seed, chunk = 0xDE0550003, 1 << 16
+    for base, length in [(0, 5 * chunk), (3 * chunk, 4 * chunk), (7 * chunk, 3 * chunk + 40)]:
+        a = oracle_lib.root_synthetic(length, chunk, seed, nthreads=3, want_leaves=True, base=base)
+        b = oracle_lib.root_buffer(oracle_lib.splitmix_bytes(length, seed, off=base), chunk, nthreads=2)
+        assert a == b, (base, length)
+    whole, _ = oracle_lib.root_synthetic(8 * chunk, chunk, seed, want_leaves=True)
+    parts = b"".join(oracle_lib.root_synthetic(2 * chunk, chunk, seed, want_leaves=True, base=r * 2 * chunk)[0]
+                     for r in range(4))
+    assert parts == whole
+    with pytest.raises(ValueError):
+        oracle_lib.root_synthetic(64, 64, 1, base=4)          # base must be a multiple of 8
+
+
 # ---- property tests (hypothesis): the C restatement == the hashlib restatement == the literal
 # merkletree v0.2.0 recursion on arbitrary chunk lists, and sharded composition == whole root
 from hypothesis import given, settings, strategies as st  # noqa: E402
