@@ -155,3 +155,33 @@ def test_configs1_ragged_full_size(ctx, oracle_lib, length):
     leaves, want = oracle_lib.root_synthetic(length, CHUNK, seed, nthreads=_threads(), want_leaves=True)
     assert got_leaves == leaves
     assert got == want, (length, got.hex(), want.hex())
+
+
+def test_new_hash_tree_257_segment_files(ctx, oracle_lib):
+    """The reference's own entry point at the headline's scale, odd: NewHashTree(chunkPath) over
+    257 files of 32 MiB (8 GiB + 32 MiB, DeOSS's segment files; types.go:19-39) through
+    dm_new_hash_tree (page cache -> pinned stripes -> K1Q, zero-copy), every leaf digest and the
+    root against the oracle's regeneration of the same bytes (file i = bytes [i, i + 1) x 32 MiB of
+    one splitmix64 stream, so the files' concatenation is one synthetic object)."""
+    import shutil
+    import tempfile
+    import numpy as np
+    nfiles, seed = 257, SEED + 1
+    need = nfiles * CHUNK + (2 << 30)
+    base = "/dev/shm" if os.path.isdir("/dev/shm") and shutil.disk_usage("/dev/shm").free > need else None
+    d = tempfile.mkdtemp(prefix="deoss_nht_", dir=base)
+    try:
+        buf = np.empty(CHUNK, dtype=np.uint8)
+        paths = []
+        for i in range(nfiles):
+            oracle_lib.fill_splitmix_ptr(buf.ctypes.data, i * CHUNK, CHUNK, seed)
+            p = os.path.join(d, f"seg{i:04d}")
+            buf.tofile(p)
+            paths.append(p)
+        leaves, root = ctx.new_hash_tree(paths)
+        want_leaves, want = oracle_lib.root_synthetic(nfiles * CHUNK, CHUNK, seed, nthreads=_threads(),
+                                                      want_leaves=True)
+        assert b"".join(leaves) == want_leaves
+        assert root == want
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
