@@ -185,3 +185,30 @@ def test_new_hash_tree_257_segment_files(ctx, oracle_lib):
         assert root == want
     finally:
         shutil.rmtree(d, ignore_errors=True)
+
+
+def test_stream_upload_full_size_odd(ctx, oracle_lib):
+    """Hash while the body arrives (dm_stream) at the headline's scale: an 8 GiB +
+    32 MiB + 8 B body (258 leaves of 32 MiB, the last 8 bytes) written in pieces of random sizes
+    (1 B .. 8 MiB, as a handler's reads of c.Request.Body return), across the stream's 1 GiB device
+    segments and batched leaf launches; every leaf digest and the root against the oracle."""
+    import random
+    import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
+    length, seed = 8 * GiB + CHUNK + 8, SEED + 1
+    host = np.empty(length, dtype=np.uint8)
+    step = 256 * MiB
+    with ThreadPoolExecutor(_threads()) as ex:
+        list(ex.map(lambda o: oracle_lib.fill_splitmix_ptr(host.ctypes.data + o, o, min(step, length - o), seed),
+                    range(0, length, step)))
+    rnd = random.Random(11)
+    st = ctx.open_stream(CHUNK)
+    pos = 0
+    while pos < length:
+        n = min(length - pos, rnd.choice([1, 7, 4096, 65536, 1 << 20, 3 << 20, 8 << 20]))
+        st.write((host.ctypes.data + pos, n))
+        pos += n
+    leaves, root = st.close(want_leaves=True)
+    want_leaves, want = oracle_lib.root_synthetic(length, CHUNK, seed, nthreads=_threads(), want_leaves=True)
+    assert leaves == want_leaves
+    assert root == want
