@@ -224,9 +224,13 @@ def main() -> None:
         torch.cuda.empty_cache()
         dist.barrier(group=wait_group)
         inproc, hung = None, False
-        progress("in-process leg (rank 0 over every GPU)")
+        progress("in-process leg (rank 0 over every GPU, in a child process)")
         if rank == 0:
-            inproc, hung = run_with_watchdog(lambda: in_process_configs(args, torch, world), args.inproc_timeout)
+            leg = ["--workload", "inprocess", "--gpus", "1", "--inproc-gib", str(args.inproc_gib)]
+            if args.same_device:
+                leg += ["--same-device", "--inproc-devices", str(world)]
+            inproc, hung = run_child_leg([sys.executable, os.path.abspath(__file__), *leg], "in_process",
+                                         args.inproc_timeout)
         flag = torch.tensor([1 if hung else 0], dtype=torch.int64)
         dist.all_reduce(flag, group=wait_group)           # doubles as the barrier
         if rank == 0:
@@ -241,9 +245,9 @@ def main() -> None:
 
 
 def exit_after_hang(out, detail):
-    """A watchdogged leg never returned (its thread may still hold GPUs or an RCCL init): rank 0
-    prints the line (ok false, the leg's error in it), then every rank leaves at once with status 3
-    -- never 0, so the driver records the hang as a failure.  No re-exec, no restart."""
+    """A watchdogged leg never returned (its child was killed): rank 0 prints the line (ok false,
+    the leg's error in it), then every rank leaves at once with status 3 -- never 0, so the driver
+    records the hang as a failure.  No re-exec, no restart."""
     if out is not None:
         emit(out, detail)
     sys.stdout.flush()
@@ -252,10 +256,11 @@ def exit_after_hang(out, detail):
 
 
 def watchdog_check(args) -> None:
-    """Hidden --watchdog-check S (tests/test_bench_launch.py): a leg that sleeps past its S-second
-    watchdog goes through the same exit path as the N = 8 in-process leg -- no GPU touched."""
+    """Hidden --watchdog-check S (tests/test_bench_line.py): a child leg that sleeps past its
+    S-second watchdog goes through the same kill and exit path as the N = 8 in-process leg -- no GPU
+    touched."""
     out = {"metric": "watchdog check", "value": 0.0, "unit": "GiB/s", "n_gpus": 1, "steps": 0, "warmup": 0}
-    r, hung = run_with_watchdog(lambda: time.sleep(60), args.watchdog_check)
+    r, hung = run_child_leg([sys.executable, "-c", "import time; time.sleep(60)"], "in_process", args.watchdog_check)
     out["other_configs"] = {"in_process": r}
     if hung:
         exit_after_hang(out, args.detail_out)
@@ -298,25 +303,48 @@ def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, 
     return res
 
 
-def run_with_watchdog(fn, timeout_s):
-    """fn() on a daemon thread, waited for at most timeout_s: (result, False), or
-    ({"error": ...}, True) when it raised / did not return in time.  The N = 8 in-process leg runs
-    this way so that a hang in it (a first RCCL init over 8 GPUs, say) cannot cost the line."""
-    import threading
-    box = {}
+DIST_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE",
+            "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT",
+            "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE", "TORCHELASTIC_ERROR_FILE")
 
-    def body():
+
+def run_child_leg(cmd, key, timeout_s):
+    """Run one leg as a child process (its own session, no rank environment) and take `key` from
+    the last JSON line it prints: (result, False); ({"error": ...}, False) when it crashed or printed
+    no result; ({"error": ...}, True) when it outlived timeout_s, after its process group was killed.
+    The N = 8 in-process leg runs this way (one dm_ctx over every GPU of the node, its own
+    ncclCommInitAll): a segfault or abort inside it cannot take rank 0's line with it, and a hang is
+    killed, so no thread of it is left holding GPUs when the ranks leave.  A child, not an exec: the
+    ranks have initialised HIP."""
+    import signal
+    env = {k: v for k, v in os.environ.items() if k not in DIST_ENV}
+    try:
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, cwd=ROOT, text=True, start_new_session=True)
+    except OSError as e:
+        return {"error": f"could not start the leg: {e}"}, False
+    try:
+        text, _ = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
         try:
-            box["r"] = fn()
-        except Exception as e:   # reported, never fatal to the headline line
-            box["r"] = {"error": f"{type(e).__name__}: {e}"}
-
-    th = threading.Thread(target=body, daemon=True)
-    th.start()
-    th.join(timeout_s)
-    if th.is_alive():
-        return {"error": f"did not finish within {timeout_s} s (watchdog)"}, True
-    return box["r"], False
+            os.killpg(p.pid, signal.SIGKILL)   # the group this call started (start_new_session), nothing else
+        except OSError:
+            pass
+        p.wait()
+        return {"error": f"did not finish within {timeout_s} s (watchdog: child process group killed)"}, True
+    for ln in reversed(text.splitlines()):
+        ln = ln.strip()
+        if not ln.startswith("{"):
+            continue
+        try:
+            d = json.loads(ln)
+        except ValueError:
+            continue
+        if isinstance(d, dict) and key in d:
+            r = d[key]
+            if p.returncode != 0 and isinstance(r, dict):
+                r = dict(r, error=f"child exited with status {p.returncode} after printing its result")
+            return r, False
+    return {"error": f"child exited with status {p.returncode} without a result"}, False
 
 
 def self_launch(n: int, argv) -> int:

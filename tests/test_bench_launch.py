@@ -70,15 +70,51 @@ def test_external_launcher_is_used_as_is():
     assert c["world_size"] == 1 and c["launcher"].startswith("external")
 
 
-def test_watchdog_returns_on_time_and_reports_hangs():
-    """run_with_watchdog (the N = 8 in-process leg's guard): a result, an exception and a hang."""
-    import threading
+def _child(code):
+    return [sys.executable, "-c", textwrap.dedent(code)]
+
+
+def test_child_leg_result_crash_and_hang(tmp_path, monkeypatch):
+    """run_child_leg (the N = 8 in-process leg's guard): a result, a crash, a crash after the
+    result, no result, and a hang whose whole process group is killed."""
+    import time
     sys.path.insert(0, ROOT)
     import bench
-    assert bench.run_with_watchdog(lambda: {"ok": 1}, 5) == ({"ok": 1}, False)
-    r, hung = bench.run_with_watchdog(lambda: 1 / 0, 5)
-    assert not hung and r["error"].startswith("ZeroDivisionError")
-    stop = threading.Event()
-    r, hung = bench.run_with_watchdog(lambda: stop.wait(30), 0.2)
-    stop.set()
-    assert hung and "watchdog" in r["error"]
+    r, hung = bench.run_child_leg(_child('print("noise"); print(\'{"in_process": {"bit_exact": true}}\')'),
+                                  "in_process", 60)
+    assert (r, hung) == ({"bit_exact": True}, False)
+    r, hung = bench.run_child_leg(_child("import os; os.abort()"), "in_process", 60)   # SIGABRT, no line
+    assert not hung and "without a result" in r["error"] and "-6" in r["error"]
+    r, hung = bench.run_child_leg(_child('print(\'{"in_process": {"bit_exact": true}}\'); raise SystemExit(7)'),
+                                  "in_process", 60)
+    assert not hung and r["bit_exact"] is True and "status 7" in r["error"]
+    # the rank environment is not handed to the leg (it would re-form the process group)
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "0")
+    r, _ = bench.run_child_leg(_child("""
+        import json, os
+        print(json.dumps({"in_process": {"env": [k for k in ("WORLD_SIZE", "RANK") if k in os.environ]}}))
+    """), "in_process", 60)
+    assert r == {"env": []}
+    # a hang: the leg and a grandchild it started are killed together
+    marker = tmp_path / "grandchild.pid"
+    t0 = time.monotonic()
+    r, hung = bench.run_child_leg(_child(f"""
+        import subprocess, sys, time
+        g = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(120)"])
+        open({str(marker)!r}, "w").write(str(g.pid))
+        time.sleep(120)
+    """), "in_process", 3)
+    assert hung and "watchdog" in r["error"] and time.monotonic() - t0 < 30
+    gpid = int(marker.read_text())
+    for _ in range(50):                      # the grandchild is gone (reaped by init) soon after the kill
+        try:
+            os.kill(gpid, 0)
+        except ProcessLookupError:
+            break
+        with open(f"/proc/{gpid}/stat") as f:
+            if f.read().split(") ")[1].startswith("Z"):
+                break
+        time.sleep(0.1)
+    else:
+        raise AssertionError("grandchild survived the watchdog kill")
