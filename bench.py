@@ -201,6 +201,9 @@ def main() -> None:
         out["parity"]["pinned_by"] = PIN_MERKLE
     if world > 1:
         out["launch"] = launch_info(torch, dist, world, rank, local_rank, dev_index, args)
+        progress("exchange: the all-gather of subtree roots alone")
+        out["exchange"] = measure_exchange(plan_shards(out["config"]["object_bytes"], args.chunk, world), torch,
+                                           dist, device, gloo, barrier)
     detail = args.detail_out or os.path.join(ROOT, "gpurun_out", f"bench_detail_n{out['n_gpus']}.json")
     if world > 1 and not args.total_gib and not args.no_strong:
         progress("strong-scaling leg: configs[1]'s 8 GiB object over every rank")
@@ -384,6 +387,32 @@ def launch_check(args) -> None:
               flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measure_exchange(plan, torch, dist, device, gloo, barrier, reps=100):
+    """N > 1: the headline step's one collective timed alone -- all_gather_into_tensor of the
+    fixed per-rank slots sharded_root sends (max nodes x 32 B per rank), `reps` back to back after
+    5 warm-ups, wall clock to the device being idle, max over ranks.  This is the measured figure
+    for the routing model's all-gather term (dm_plan::route, an estimate of 0.1 ms until a
+    multi-GPU node runs this)."""
+    slot = plan.max_nodes * 32
+    comm = "cpu" if gloo else device
+    send = torch.zeros(slot, dtype=torch.uint8, device=comm)
+    gathered = torch.empty(plan.world * slot, dtype=torch.uint8, device=comm)
+    for _ in range(5):
+        dist.all_gather_into_tensor(gathered, send)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_gather_into_tensor(gathered, send)
+    if not gloo:
+        torch.cuda.synchronize()   # RCCL runs on its own stream; gloo returns when done
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=comm)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return {"collective": "all_gather_into_tensor", "backend": "gloo" if gloo else "nccl (RCCL)",
+            "bytes_per_rank": slot, "ranks": plan.world, "reps": reps,
+            "avg_us": round(float(t.item()) / reps * 1e6, 2)}
 
 
 def launch_info(torch, dist, world, rank, local_rank, dev_index, args):
@@ -747,6 +776,9 @@ def compact_line(out, detail_path=None):
         line["launch"] = {k: la.get(k) for k in ("world_size", "backend", "device_count", "distinct_gpus",
                                                  "rccl_version", "launcher")}
         line["launch"]["launcher"] = _short(la.get("launcher"), 60)
+    ex = out.get("exchange")
+    if isinstance(ex, dict):
+        line["exchange"] = {k: ex.get(k) for k in ("backend", "bytes_per_rank", "ranks", "avg_us")}
     for k in ("same_device", "note", "ranks"):
         if k in out:
             line[k] = out[k]

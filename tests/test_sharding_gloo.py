@@ -148,3 +148,31 @@ def test_plan_properties():
     plan = plan_shards(1 << 40, 32 << 20, 8)
     assert plan.k == 12 and plan.n_blocks == 8
     assert all(plan.byte_range(r) == (r << 37, (r + 1) << 37) for r in range(8))
+
+
+def _exchange_worker(rank, world, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        import bench
+        plan = plan_shards(world * (8 << 30), 32 << 20, world)      # the weak-scaling headline's layout
+        r = bench.measure_exchange(plan, torch, dist, "cpu", True, dist.barrier, reps=20)
+        if rank == 0:
+            results.append(r)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_exchange_timing_gloo(world):
+    """bench.measure_exchange (the N > 1 line's `exchange`): the headline's all-gather alone, on
+    every rank, max over ranks -- one 32-byte subtree root per rank at the weak-scaling layout."""
+    mgr = mp.Manager()
+    results = mgr.list()
+    mp.spawn(_exchange_worker, args=(world, _free_port(), results), nprocs=world, join=True)
+    (r,) = list(results)
+    assert r["bytes_per_rank"] == 32 and r["ranks"] == world and r["reps"] == 20
+    assert r["backend"] == "gloo" and 0 < r["avg_us"] < 1e6
