@@ -107,12 +107,12 @@ def sharded_root(plan: ShardPlan, rank: int, local_subtree: Callable[[int], "obj
     dist_mod.all_gather_into_tensor(gathered, send, group=group)
     if rank != 0:
         return None
-    parts: List = []
-    for r in range(plan.world):
-        c = plan.node_count(r)
-        if c:
-            parts.append(gathered[r * slot:r * slot + c * 32])
-    nodes = parts[0] if len(parts) == 1 else torch_mod.cat(parts)
+    counts = [plan.node_count(r) for r in range(plan.world)]
+    if all(c * 32 == slot for c in counts):
+        nodes = gathered             # every slot full (one block per rank, the bench layouts): no copy
+    else:
+        parts: List = [gathered[r * slot:r * slot + c * 32] for r, c in enumerate(counts) if c]
+        nodes = parts[0] if len(parts) == 1 else torch_mod.cat(parts)
     if str(comm) != str(device):
         nodes = nodes.to(device)
     return finish(nodes, plan.n_blocks, plan.k == 0)
