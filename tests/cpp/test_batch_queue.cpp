@@ -8,6 +8,7 @@
 //  - a queue whose oldest request has already waited launches at once;
 //  - a queue that holds a full batch by the byte budget (leaves to spare) launches at once;
 //  - stop() drains what is queued, then refuses new requests.
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -134,19 +135,37 @@ static void test_burst_while_busy() {
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
     const int n = 24;
     std::vector<TReq> burst(n);
+    std::vector<clk::time_point> sent(n);
     std::vector<std::thread> th;
+    // threads exist before the burst starts (thread creation under TSan on a loaded host takes
+    // milliseconds); each submits at start + i x 0.25 ms
+    std::atomic<bool> go{false};
+    clk::time_point start;
     for (int i = 0; i < n; i++) {
         burst[i].id = 100 + i;
         burst[i].leaves = 13;
         burst[i].chain_bytes = 32 << 20;
-        th.emplace_back([&, i] { q.submit(burst[i]); });
-        std::this_thread::sleep_for(std::chrono::microseconds(250));
+        th.emplace_back([&, i] {
+            while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+            std::this_thread::sleep_until(start + std::chrono::microseconds(250 * i));
+            sent[i] = clk::now();
+            q.submit(burst[i]);
+        });
     }
+    start = clk::now();
+    go.store(true, std::memory_order_release);
     for (auto& t : th) t.join();
     t1.join();
     const dm_batch::Stats st = q.stats();
-    // 1 batch for `first`, and the burst in at most 3 more (it never waits a whole 120 ms batch)
-    EXPECT(st.batches <= 4, "burst of %d cut into %llu batches", n, (unsigned long long)st.batches - 1);
+    const double spread_ms =
+        std::chrono::duration<double, std::milli>(*std::max_element(sent.begin(), sent.end()) - start).count();
+    if (spread_ms > 8.0) {   // the host could not deliver the burst in its ~6 ms: the premise did not hold
+        std::printf("note: burst arrived over %.1f ms (planned 6): batch-count check skipped\n", spread_ms);
+    } else {
+        // 1 batch for `first`, and the burst in at most 3 more (it never waits a whole 120 ms batch)
+        EXPECT(st.batches <= 4, "burst of %d cut into %llu batches (arrived over %.1f ms)", n,
+               (unsigned long long)st.batches - 1, spread_ms);
+    }
     pool.join();
 }
 
