@@ -264,11 +264,11 @@ struct Reaper {
                 q.pop_front();
                 active++;
             }
-            if (hipSetDevice(it.dev) == hipSuccess) {
-                if (it.pinned) host_release(it.p);
-                else dev_release(it.dev, it.p);
-            }
+            // hipFree resolves the allocation from the pointer; a failed hipSetDevice must not leak it
+            (void)hipSetDevice(it.dev);
             (void)hipGetLastError();
+            if (it.pinned) host_release(it.p);
+            else dev_release(it.dev, it.p);
             {
                 std::lock_guard<std::mutex> lk(mu);
                 active--;
