@@ -706,6 +706,10 @@ def _in_process_line(r):
     x = (r.get("sharded_object") or {}).get("exchange") or {}
     if x:
         e["exchange_avg_us"] = x.get("avg_us")
+    hf = r.get("host_feed")
+    if isinstance(hf, dict):
+        e["host_feed"] = ({k: hf.get(k) for k in ("alone_GBps", "all_GBps", "consistent")} if "error" not in hf
+                          else {"error": _short(hf["error"], 120)})
     e["ok"] = r.get("bit_exact") is True
     return e
 

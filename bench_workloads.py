@@ -427,6 +427,16 @@ def in_process_configs(args, torch, world):
         except Exception as e:
             leg["error"] = f"{type(e).__name__}: {e}"
         res["concurrent_calls"] = leg
+
+        # d. the host feed: PCIe reads of pinned host memory, one GPU alone, then every GPU at once
+        leg = {"what": "dm_read_probe_async over the pinned object (zero-copy reads over PCIe): GPU 0 reads its "
+                       "slice alone, then every GPU its own slice at once -- the routing model's host-memory "
+                       "bandwidth term (dm_plan::route, an estimate of 500 GB/s until measured; DESIGN.md §7)"}
+        try:
+            leg.update(_host_feed(ctx, torch, pin.ptr, size, ndev, virtual))
+        except Exception as e:
+            leg["error"] = f"{type(e).__name__}: {e}"
+        res["host_feed"] = leg
         ctx.close()
     finally:
         pin.free()
@@ -435,6 +445,44 @@ def in_process_configs(args, torch, world):
     if virtual:
         res["note"] = "rehearsal: virtual devices on one GPU (D2D gather); not a multi-GPU result"
     return res
+
+
+def _host_feed(ctx, torch, host_ptr, size, ndev, virtual, reps=3):
+    """Zero-copy PCIe read rate of pinned host memory (in_process_configs leg d): each device reads
+    an equal slice of the object with the library's read probe (XOR of every 16-byte word, one
+    pass), on a stream of its own; GPU 0 alone, then every device at once.  Best of `reps`, wall
+    clock from the first launch to the last stream idle.  The all-device XOR of slice 0 must equal
+    the alone one (the same bytes read twice)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    dp = ctypes.c_void_p()
+    rc = hip.hipHostGetDevicePointer(ctypes.byref(dp), ctypes.c_void_p(host_ptr), 0)
+    if rc != 0 or not dp.value:
+        raise RuntimeError(f"hipHostGetDevicePointer returned {rc}")
+    sl = size // ndev // 16 * 16
+    gpu = [0] * ndev if virtual else list(range(ndev))
+    xs = [torch.zeros(1, dtype=torch.int64, device=f"cuda:{g}") for g in gpu]
+    streams = [torch.cuda.Stream(device=f"cuda:{g}") for g in gpu]
+
+    def run(idx):
+        for g in sorted(set(gpu)):
+            torch.cuda.synchronize(g)
+        t = time.perf_counter()
+        for i in idx:
+            ctx.read_probe_async(dp.value + i * sl, sl, xs[i].data_ptr(), streams[i].cuda_stream)
+        for i in idx:
+            streams[i].synchronize()
+        return time.perf_counter() - t
+
+    run([0])                                         # warm: the probe's first launch on each device
+    alone = min(run([0]) for _ in range(reps))
+    x_alone = int(xs[0].item())
+    every = min(run(list(range(ndev))) for _ in range(reps))
+    return {"slice_bytes": sl, "devices": ndev, "alone_GBps": round(sl / alone / 1e9, 2),
+            "all_GBps": round(ndev * sl / every / 1e9, 2), "all_ms": round(every * 1e3, 2),
+            "consistent": int(xs[0].item()) == x_alone,
+            "note": "virtual devices share one GPU's link: not a multi-GPU figure" if virtual else
+                    "aggregate host-to-GPU zero-copy read rate of this node"}
 
 
 def _summary(r):

@@ -31,3 +31,6 @@ def test_in_process_leg_virtual_devices():
     assert b["parity"]["checked_objects"] == b["objects"] > 0 and b["parity"]["mismatches"] == 0
     c = res["concurrent_calls"]
     assert c["parity"]["checked_calls"] == 8 and len(c["gpus_used"]) >= 2   # routed over the devices
+    h = res["host_feed"]
+    assert "error" not in h, h
+    assert h["devices"] == 4 and h["consistent"] and h["alone_GBps"] > 1 and h["all_GBps"] > 1
