@@ -27,7 +27,7 @@ DM_ERR_NODEV = -7
 # Every symbol include/deoss_merkle.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = (
     "dm_create", "dm_create_lanes", "dm_destroy", "dm_strerror", "dm_last_error", "dm_device_count",
-    "dm_lane_count", "dm_gpu_count", "dm_keep_claimed",
+    "dm_lane_count", "dm_gpu_count", "dm_keep_claimed", "dm_can_shard",
     "dm_new_hash_tree", "dm_root_chunks", "dm_root_buffer", "dm_root_batch",
     "dm_root_device", "dm_root_device_async", "dm_subtree_device_async", "dm_finish_device_async",
     "dm_root_batch_device_async", "dm_fill_synthetic_async", "dm_read_probe_async", "dm_host_alloc",
@@ -71,6 +71,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_device_count": ([vp], i32),
         "dm_gpu_count": ([], i32),
         "dm_keep_claimed": ([i32, pu64], i32),
+        "dm_can_shard": ([vp], i32),
         "dm_new_hash_tree": ([vp, ctypes.POINTER(ctypes.c_char_p), u64, vp, vp], i32),
         "dm_root_chunks": ([vp, pvp, pu64, u64, vp, vp], i32),
         "dm_root_buffer": ([vp, vp, u64, u64, vp, vp], i32),

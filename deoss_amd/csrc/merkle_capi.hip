@@ -371,6 +371,10 @@ struct dm_ctx {
     // compaction and the batch split run with G = N on a one-GPU box.  RCCL rejects duplicate
     // GPUs, so the gather of subtree roots is then a D2D copy to device 0 (real GPUs: RCCL).
     bool virtual_devs = false;
+    // false when ncclCommInitAll failed at dm_create on an unforced multi-GPU context: every call
+    // then runs whole on one GPU (routing never shards an object; batches still split by objects,
+    // which needs no exchange) instead of the context failing outright.
+    bool shard_ok = true;
     bool keep_claimed = false;             // its lanes' keep bytes count in g_keep_claimed (dm_create)
     // Exchange timing of multi-device calls while timing is on (dm_exchange_timing): host clock
     // from every device's subtree roots being ready to the gathered slots being on every device.
@@ -1433,7 +1437,7 @@ int host_src(const void* p) {
 int route_call(dm_ctx* c, uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, bool by_objects = false) {
     const int G = c->nphys;   // GPUs; a call never shards over lanes of one GPU
     if (c->force_sharded) return n >= 2 * (uint64_t)G ? G : 1;
-    if (G <= 1) return 1;
+    if (G <= 1 || (!c->shard_ok && !by_objects)) return 1;
     return dm_plan::route(n, bytes, leaf_max, src, G, c->devs[0].cus, c->leaf_mode.load(), ctx_load(c), by_objects);
 }
 
@@ -1612,6 +1616,14 @@ int default_lanes(int dev) {
     return (int)std::min<uint64_t>(std::max<uint64_t>(std::min(by_free, by_budget), 1), 4);
 }
 
+// An unforced multi-GPU context whose RCCL communicators could not be created keeps working with
+// every call whole on one GPU (dm_ctx::shard_ok); said once on stderr, queryable (dm_can_shard).
+void no_sharding(dm_ctx* c, const char* why) {
+    c->shard_ok = false;
+    std::fprintf(stderr, "deoss_merkle: RCCL communicators over %d GPUs unavailable (%s); every call runs whole on "
+                 "one GPU\n", c->nphys, why);
+}
+
 int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
     if (!out || lanes < 1 || lanes > kMaxLanes) return bad_arg();
     *out = nullptr;
@@ -1655,11 +1667,22 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
     if ((ids.size() > 1 || c->force_sharded) && !c->virtual_devs) {   // every device's communicator up front: fail here, not mid-call
         std::vector<ncclComm_t>* cm = nullptr;
         const int rc = comms_for(c, (int)ids.size(), &cm);
-        if (rc != DM_OK) {
+        if (rc != DM_OK && c->force_sharded) {
             dm_destroy(c);
             return set_err(DM_ERR_RCCL, "ncclCommInitAll failed");
         }
+        if (rc != DM_OK) {   // sharding is an optimisation: keep the context, never shard an object
+            std::string why;
+            {
+                std::lock_guard<std::mutex> lk(c->err_mu);
+                why.swap(c->err);
+            }
+            t_err.clear();
+            no_sharding(c, why.c_str());
+        }
     }
+    const char* tf = std::getenv("DEOSS_TEST_RCCL_INIT_FAIL");   // test hook: the degraded path on one GPU
+    if (tf && tf[0] == '1' && ids.size() > 1 && !c->force_sharded) no_sharding(c, "DEOSS_TEST_RCCL_INIT_FAIL=1");
     *out = c;
     return DM_OK;
 }
@@ -1682,6 +1705,8 @@ int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) {
     std::lock_guard<std::mutex> lk(g_create_mu);
     return ctx_create(out, devs, ndev, lanes);
 }
+
+int dm_can_shard(dm_ctx* ctx) { return ctx && ctx->nphys > 1 && (ctx->shard_ok || ctx->force_sharded) ? 1 : 0; }
 
 int dm_keep_claimed(int hip_device, uint64_t* bytes) {
     if (!bytes || hip_device < 0) return bad_arg();

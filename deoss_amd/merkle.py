@@ -62,6 +62,13 @@ class MerkleContext:
     def lane_count(self) -> int:
         return self._L.dm_lane_count(self._h)
 
+    @property
+    def can_shard(self) -> bool:
+        """Whether one object can be sharded over this context's GPUs (dm_can_shard): more than one
+        GPU and RCCL communicators up.  A context whose RCCL init failed runs every call whole on
+        one GPU."""
+        return bool(self._L.dm_can_shard(self._h))
+
     @staticmethod
     def keep_claimed(hip_device: int = 0) -> int:
         """Idle lane-buffer bytes every live context of this process may keep on that GPU

@@ -91,6 +91,11 @@ int dm_gpu_count(void);
  * (sum over their lanes on it of the per-lane keep limit): the budget dm_create sizes its default
  * lane count against.  0 on success. */
 int dm_keep_claimed(int hip_device, uint64_t *bytes);
+/* 1 when the context can shard one object over its GPUs (more than one GPU and its RCCL
+ * communicators up), else 0.  A multi-GPU dm_create whose ncclCommInitAll fails still succeeds:
+ * the context then runs every call whole on one GPU (batches still split by objects, which needs
+ * no exchange), says so once on stderr, and answers 0 here. */
+int dm_can_shard(dm_ctx *ctx);
 
 /* Page-locked host memory, visible to every GPU, for callers that want the zero-copy host paths.
  * dm_root_buffer / dm_root_chunks / dm_root_batch hash an object held in such memory in place: K1Q

@@ -511,6 +511,42 @@ def test_virtual_devices_sharded_paths(oracle_lib, tmp_path, G):
         c.close()
 
 
+def test_rccl_init_failure_degrades_to_one_gpu(oracle_lib, monkeypatch, capfd):
+    """A multi-GPU context whose RCCL communicators cannot be created (DEOSS_TEST_RCCL_INIT_FAIL
+    stands in for ncclCommInitAll failing) still works: dm_create succeeds, says so on stderr,
+    dm_can_shard is 0, and a call the router would otherwise shard over every device (1 GiB of
+    pinned host memory at 64 KiB chunks over 4 devices) runs whole on one device with the oracle's
+    root; a batch still splits by objects (no exchange).  A healthy context shards the same call."""
+    import numpy as np
+    from deoss_amd import MerkleContext, PinnedBuffer
+    data = oracle_lib.splitmix_bytes(1 << 30, 0xDE6)
+    _, want = oracle_lib.root_buffer(data, 1 << 16, nthreads=16)
+    pin = PinnedBuffer(len(data))
+    pin.array()[:] = np.frombuffer(data, dtype=np.uint8)
+    objs = [data[i << 22:(i << 22) + (3 << 20) + i] for i in range(12)]
+    try:
+        healthy = _virtual_context(4, sharded=False)
+        try:
+            assert healthy.can_shard
+            assert healthy.root_buffer_ptr(pin.ptr, len(data), 1 << 16)[1] == want
+            assert sorted(healthy.last_call_devices()[0]) == [0, 1, 2, 3]     # routed over every device
+        finally:
+            healthy.close()
+        monkeypatch.setenv("DEOSS_TEST_RCCL_INIT_FAIL", "1")
+        capfd.readouterr()
+        c = _virtual_context(4, sharded=False)
+        try:
+            assert "RCCL communicators over 4 GPUs unavailable" in capfd.readouterr().err
+            assert c.device_count == 4 and not c.can_shard
+            assert c.root_buffer_ptr(pin.ptr, len(data), 1 << 16)[1] == want
+            assert len(c.last_call_devices()[0]) == 1                          # whole on one device
+            assert c.root_batch(objs, 1 << 20) == [oracle_lib.root_buffer(o, 1 << 20)[1] for o in objs]
+        finally:
+            c.close()
+    finally:
+        pin.free()
+
+
 def test_virtual_devices_concurrent_routing(oracle_lib):
     """Per-device locks and least-busy routing: 16 threads mixing host buffers, chunk lists,
     streams and batches on a 4-device context (one GPU) get the oracle's roots."""
