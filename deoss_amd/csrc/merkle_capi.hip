@@ -345,6 +345,11 @@ struct DevSlot {
     std::vector<StreamKit*> kits;          // idle stream kits of this device
 };
 
+inline uint64_t next_ctx_serial() {
+    static std::atomic<uint64_t> n{0};
+    return ++n;
+}
+
 struct dm_ctx {
     // Call lanes: devs holds `lanes` entries per GPU, lane-major (devs[l * nphys + p] is lane l of
     // GPU p), each with its own streams, scratch and lock, so up to `lanes` calls run on one GPU at
@@ -375,6 +380,8 @@ struct dm_ctx {
     // then runs whole on one GPU (routing never shards an object; batches still split by objects,
     // which needs no exchange) instead of the context failing outright.
     bool shard_ok = true;
+    // process-unique, never reused (dm_last_call_devices' thread-local record names it)
+    const uint64_t serial = next_ctx_serial();
     bool keep_claimed = false;             // its lanes' keep bytes count in g_keep_claimed (dm_create)
     // Exchange timing of multi-device calls while timing is on (dm_exchange_timing): host clock
     // from every device's subtree roots being ready to the gathered slots being on every device.
@@ -402,10 +409,12 @@ int bad_arg() { return set_err(DM_ERR_INVALID, "invalid argument"); }
 // indices (one for a whole call, [0, G) for a call sharded over G GPUs) and the lane.
 thread_local std::vector<int> t_call_devs;
 thread_local int t_call_lane = -1;
-thread_local const dm_ctx* t_call_ctx = nullptr;
+// the context is named by its serial (dm_ctx::serial), not its address: a context created where a
+// destroyed one lived must not see that one's last call
+thread_local uint64_t t_call_ctx = 0;
 
 void note_call(const dm_ctx* c, int g, int G) {
-    t_call_ctx = c;
+    t_call_ctx = c->serial;
     t_call_devs.clear();
     if (G == 1) {
         t_call_devs.push_back(g % c->nphys);
@@ -1768,7 +1777,7 @@ int dm_exchange_timing(dm_ctx* ctx, uint64_t* n, double* us_sum, double* us_max,
 
 int dm_last_call_devices(dm_ctx* ctx, int* devs, int* hip_ids, int cap, int* lane) {
     if (!ctx || cap < 0) return bad_arg();
-    if (t_call_ctx != ctx) {   // no call of this context on this thread yet
+    if (t_call_ctx != ctx->serial) {   // no call of this context on this thread yet
         if (lane) *lane = -1;
         return 0;
     }
