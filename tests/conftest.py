@@ -37,3 +37,13 @@ def ctx():
     c = MerkleContext()
     yield c
     c.close()
+
+
+def pytest_collection_modifyitems(config, items):
+    """DEOSS_TEST_SHUFFLE=<seed>: run the collected tests in a seeded random order (an order-
+    dependence check: a context created at a destroyed one's address once read its stale state).
+    Unset: the normal order."""
+    seed = os.environ.get("DEOSS_TEST_SHUFFLE")
+    if seed:
+        import random
+        random.Random(int(seed)).shuffle(items)
