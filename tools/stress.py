@@ -4,7 +4,9 @@ T threads for S seconds, each looping over random operations on a shared context
 batcher and contexts of their own that they create and destroy mid-run:
   pageable / pinned dm_root_buffer, dm_root_chunks, dm_root_batch, a streamed upload in random
   pieces, a device-resident root on the thread's own torch stream, a batcher root, FullProcessing
-  (1 MiB segments) on the shared context and through a PROCESS batcher, a short-lived
+  (1 MiB segments) on the shared context, from a file, while the body arrives and through a
+  PROCESS batcher, a fragment found by name, NewHashTree over chunk files, Reed-Solomon 4 + 8, a
+  short-lived
   context (create, one call, destroy), a context destroyed while another thread's calls run on
   the shared one.
 Objects come from a fixed pool whose roots the oracle computed up front, so a check is a lookup.
@@ -16,7 +18,9 @@ from __future__ import annotations
 import json
 import os
 import random
+import shutil
 import sys
+import tempfile
 import threading
 import time
 
@@ -44,7 +48,8 @@ def main():
         n = rnd.choice([1, 63, 64, 4097, 100_000, 1 << 20, (3 << 20) + 5, 9 << 20, (24 << 20) - 3])
         data = orc.splitmix_bytes(n, 500 + i)
         want = {c: orc.root_buffer(data, c, nthreads=8)[1] for c in CH}
-        want["fid"] = orc.full_processing(data, SEG, nthreads=8)[2]     # FullProcessing at 1 MiB segments
+        _, fr, want["fid"], _ = orc.full_processing(data, SEG, nthreads=8)   # FullProcessing at 1 MiB segments
+        want["frags"] = fr
         pool.append((data, want))
     big = max(len(d) for d, _ in pool)
     pin = PinnedBuffer(big * 2)
@@ -53,6 +58,8 @@ def main():
     batcher = Batcher(B_ROOT, 65536, linger_us=500)
     pbatcher = Batcher(B_PROCESS, SEG, linger_us=500)
     proc = Processor(shared, 4, 8, SEG)
+    from deoss_amd.reedsolomon import New as rs_new
+    rse = rs_new(shared, 4, 8)
     counts, fails = {}, []
     mu = threading.Lock()
     stop_at = time.perf_counter() + S
@@ -67,6 +74,7 @@ def main():
 
     def worker(t):
         r = random.Random(100 + t)
+        tmp = tempfile.mkdtemp(prefix=f"stress{t}_")
         stream = torch.cuda.Stream()
         own = None
         while time.perf_counter() < stop_at:
@@ -74,7 +82,8 @@ def main():
             c = r.choice(CH)
             want = roots[c]
             op = r.choice(["pageable", "pinned", "chunks", "batch", "stream", "device", "batcher", "short_ctx",
-                           "own_ctx", "process", "process_batcher"])
+                           "own_ctx", "process", "process_batcher", "files", "fullproc_file", "pstream", "lookup",
+                           "rs"])
             try:
                 if op == "pageable":
                     got = shared.root_buffer(data, c, want_leaves=False)[1]
@@ -113,6 +122,49 @@ def main():
                 elif op == "process_batcher":
                     want = roots["fid"]
                     got = pbatcher.process(data)[2]
+                elif op == "files":      # NewHashTree over chunk files
+                    c = 1 << 20
+                    want = roots[c]
+                    paths = []
+                    for j, o in enumerate(range(0, len(data), c)):
+                        paths.append(os.path.join(tmp, f"c{j}"))
+                        with open(paths[-1], "wb") as f:
+                            f.write(data[o:o + c])
+                    got = shared.new_hash_tree(paths)[1]
+                elif op in ("fullproc_file", "lookup"):
+                    want = roots["fid"] if op == "fullproc_file" else True
+                    src = os.path.join(tmp, "obj")
+                    with open(src, "wb") as f:
+                        f.write(data)
+                    if op == "fullproc_file":
+                        got = proc.full_processing_file(src, tmp, segment_files=False)[2]
+                        for name in os.listdir(tmp):
+                            if len(name) == 64:
+                                os.unlink(os.path.join(tmp, name))
+                    else:   # the download path: one fragment found by name, nothing written
+                        frs = roots["frags"]
+                        t_ = r.randrange(len(frs) // 32)
+                        hit = proc.fragment_lookup(src, frs[32 * t_:32 * t_ + 32].hex(), want_bytes=False)
+                        h_ = hit[0] * 12 + hit[1] if hit is not None else -1   # equal names: the first match
+                        got = h_ >= 0 and frs[32 * h_:32 * h_ + 32] == frs[32 * t_:32 * t_ + 32]
+                elif op == "pstream":    # FullProcessing while the body arrives
+                    want = roots["fid"]
+                    ps = proc.NewProcessingStream(tmp, segment_files=False)
+                    pos = 0
+                    while pos < len(data):
+                        k = r.choice([1000, 65536, 1 << 20, 3 << 20])
+                        ps.write(data[pos:pos + k])
+                        pos += k
+                    got = ps.close()[1]
+                    got = bytes.fromhex(got)
+                    for name in os.listdir(tmp):
+                        if len(name) == 64:
+                            os.unlink(os.path.join(tmp, name))
+                elif op == "rs":         # Reed-Solomon 4 + 8 of four random-length shards
+                    sz = r.choice([16, 4096, 65536, 1 << 20])
+                    shards = [data[:sz].ljust(sz, b"\0")] + [orc.splitmix_bytes(sz, 77 + j) for j in range(3)]
+                    want = orc.rs_encode(shards, 8)
+                    got = rse.Encode(shards + [bytes(sz)] * 8)[4:]
                 elif op == "short_ctx":
                     with MerkleContext(lanes=1) as x:
                         got = x.root_buffer(data, c, want_leaves=False)[1]
@@ -128,6 +180,7 @@ def main():
                 note(op, False, f"{type(e).__name__}: {e}")
         if own is not None:
             own.close()
+        shutil.rmtree(tmp, ignore_errors=True)
 
     t0 = time.perf_counter()
     th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
@@ -147,6 +200,7 @@ def main():
     batcher.close()
     pbatcher.close()
     proc.close()
+    rse.close()
     shared.close()
     pin.free()
     print(json.dumps({"threads": T, "seconds": round(wall, 1), "ops": sum(counts.values()), "by_op": counts,
