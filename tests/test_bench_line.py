@@ -68,8 +68,15 @@ def test_compact_line_n8_rehearsal():
                                    "8 GPUs", "chunk": 4096, "value": 5000.0, "unit": "GiB/s", "ms_per_step": 1.6,
                                    "bit_exact": True, "single_gpu_ms": 5.6, "speedup_vs_one_gpu": 3.5,
                                    "note": "throughput regime"}
+    full["exchange"] = {"collective": "all_gather_into_tensor", "backend": "nccl (RCCL)", "bytes_per_rank": 32,
+                        "ranks": 8, "reps": 100, "avg_us": 41.5}
+    full["other_configs"]["in_process"]["host_feed"] = {"slice_bytes": 8 << 30, "devices": 8, "alone_GBps": 56.1,
+                                                        "all_GBps": 401.7, "all_ms": 171.0, "consistent": True,
+                                                        "what": "x" * 300}
     line = bench.compact_line(full, None)
     assert _size(line) <= bench.LINE_MAX_BYTES
+    assert line["exchange"] == {"backend": "nccl (RCCL)", "bytes_per_rank": 32, "ranks": 8, "avg_us": 41.5}
+    assert line["extras"]["in_process"]["host_feed"] == {"alone_GBps": 56.1, "all_GBps": 401.7, "consistent": True}
     assert line["strong_scaling_4KiB"]["speedup_vs_one_gpu"] == 3.5 and "note" not in line["strong_scaling_4KiB"]
     for k in REQUIRED + ("parity", "launch", "extras", "strong_scaling"):
         assert k in line, k
