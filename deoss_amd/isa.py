@@ -141,7 +141,8 @@ def analyse_split(asm: str, sym: str) -> dict:
     return {"consumer": _summary(cons, 1), "producer": _summary(prod, 1)}
 
 
-def generate() -> dict:
+def generate(write: bool = True) -> dict:
+    """ISA counts of a fresh -save-temps build of the library; written to COUNTS unless write=False."""
     from . import build as b
     with tempfile.TemporaryDirectory() as td:
         out = os.path.join(td, "lib.so")
@@ -163,8 +164,9 @@ def generate() -> dict:
         d["lanes_per_leaf_block"] = {"consumer": lanes[0], "producer": lanes[1]}
         res[name] = d
     res["per"] = "one 64-byte block of one leaf"
-    with open(COUNTS, "w") as f:
-        json.dump(res, f, indent=1)
+    if write:
+        with open(COUNTS, "w") as f:
+            json.dump(res, f, indent=1)
     return res
 
 
