@@ -68,6 +68,29 @@ def test_new_hash_tree_reference_kat(tmp_path):
     assert roothashs.hex() == "b513419286835c1e36fa520b86cbf37650db82e73f510f0e6a699cc0505f1151"
 
 
+def test_merkletree_upstream_kat(ctx, tmp_path):
+    """merkletree v0.2.0's own TestNewTree SHA-256 rows (recalled from upstream, not reference-held;
+    tests/golden/merkletree_upstream_kat.json: 4 and 8 leaves) through the HIP path: chunk lists
+    and NewHashTree over one file per content."""
+    import json
+    from deoss_amd import NewHashTree
+    with open(os.path.join(os.path.dirname(__file__), "golden", "merkletree_upstream_kat.json")) as f:
+        kat = json.load(f)
+    for c in kat["cases"]:
+        chunks = [x.encode() for x in c["contents"]]
+        want = bytes(c["root"])
+        leaves, root = ctx.root_chunks(chunks)
+        assert root == want, c["id"]
+        assert leaves == b"".join(hashlib.sha256(x).digest() for x in chunks)
+        paths = []
+        for i, x in enumerate(chunks):
+            p = tmp_path / f"kat{c['id']}_{i}"
+            p.write_bytes(x)
+            paths.append(str(p))
+        tree, err = NewHashTree(paths, ctx=ctx)
+        assert err is None and tree.MerkleRoot() == want, c["id"]
+
+
 def test_go_stream_mirror():
     """NewStream / Write / Close / Abort as the Go package exposes them (go/hashtree/stream_hip.go)."""
     from deoss_amd import Init, NewHashTreeFromBuffer, NewStream

@@ -1,10 +1,14 @@
 """CPU tests pinning the oracle (oracle/) before it is trusted as the GPU checker."""
 import hashlib
+import json
+import os
 import random
 
 import pytest
 
 from oracle import (py_go_tree, py_reduce, py_root_chunks, split_chunks, splitmix64_bytes)
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def chunks_of(case):
@@ -216,3 +220,18 @@ def test_property_sharded_levels_compose(n, world, seed):
             nodes.extend(part)
     finished = py_reduce(nodes) if (plan.k == 0 or len(nodes) > 1) else nodes
     assert finished[0] == py_reduce(digests)[0]
+
+
+def test_merkletree_upstream_kat(oracle_lib):
+    """merkletree v0.2.0's own TestNewTree SHA-256 rows (recalled from upstream, not reference-held;
+    tests/golden/merkletree_upstream_kat.json): the C restatement, the hashlib restatement and the
+    literal Go recursion all give the upstream roots (4 and 8 leaves)."""
+    from oracle import py_go_tree
+    with open(os.path.join(ROOT, "tests", "golden", "merkletree_upstream_kat.json")) as f:
+        kat = json.load(f)
+    for c in kat["cases"]:
+        chunks = [x.encode() for x in c["contents"]]
+        want = bytes(c["root"])
+        assert oracle_lib.root_chunks(chunks)[1] == want, c["id"]
+        assert py_root_chunks(chunks)[1] == want, c["id"]
+        assert py_go_tree(chunks)[1] == want, c["id"]
