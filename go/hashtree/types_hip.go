@@ -105,6 +105,17 @@ func gpu() (*C.dm_ctx, error) {
 	return ctx, ctxErr
 }
 
+// Sharding reports whether the package's context can shard one object over its GPUs: more than
+// one GPU and RCCL communicators up.  A node whose RCCL init failed still hashes, every call whole
+// on one GPU (dm_can_shard; the library says so once on stderr).
+func Sharding() (bool, error) {
+	c, err := gpu()
+	if err != nil {
+		return false, err
+	}
+	return C.dm_can_shard(c) == 1, nil
+}
+
 // rcError reads the library's thread-local message of the failing call: the caller holds
 // runtime.LockOSThread from the call until here.
 func rcError(c *C.dm_ctx, rc C.int) error {
