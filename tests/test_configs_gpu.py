@@ -10,7 +10,8 @@ bench.py).  The oracle is the checker only; every result comes from libdeoss_mer
   configs[3]  one GPU's share of the 1 TiB object: 4,096 x 32 MiB leaves (128 GiB) generated in
               HBM at the share's byte offset, reduced 12 levels by dm_subtree_device_async (the
               block root that rank sends in the RCCL all-gather), against the oracle's root of
-              the same leaf range regenerated leaf by leaf (or_root_synthetic_at).
+              the same leaf range regenerated leaf by leaf (or_root_synthetic_at); and the whole
+              1 TiB object share by share on one GPU against the full-size fixture.
   configs[1]  the 8 GiB object made ragged at full size (257 / 256 / 255 leaves with short last
               leaves): merkletree's odd-count duplication at the headline's scale, leaves and root.
 
@@ -129,6 +130,40 @@ def test_configs3_share_4096x32MiB_subtree(ctx, oracle_lib):
     torch.cuda.empty_cache()
     _, want = oracle_lib.root_synthetic(share, CHUNK, seed, nthreads=_threads(), base=off)
     assert got == want
+
+
+def test_configs3_full_object_shard_by_shard_on_one_gpu(ctx):
+    """The whole 1 TiB configs[3] object on ONE MI355X, as the 8-GPU run computes it, one rank's
+    share after another: each 128 GiB share generated in HBM at its byte offset (bench.py's seed,
+    the bytes the N = 8 line's configs[3] hashes), 4,096 leaves reduced 12 levels to that rank's
+    block root (dm_subtree_device_async), then the 8 block roots finished to the root
+    (dm_finish_device_async, what rank 0 does after the RCCL all-gather).  Every block root and
+    the root equal the oracle's full-size fixture (tests/golden/config3_root.json, 32,768 leaves
+    regenerated leaf by leaf by tests/golden/make_config3_root.py)."""
+    import json
+    torch = _torch()
+    with open(os.path.join(os.path.dirname(__file__), "golden", "config3_root.json")) as f:
+        fx = json.load(f)
+    share, ranks = 128 * GiB, 8
+    assert fx["len"] == ranks * share and fx["chunk"] == CHUNK
+    _need_hbm(torch, share + 4 * GiB)
+    buf = torch.empty(share + 64, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    nodes = torch.zeros(ranks * 32, dtype=torch.uint8, device="cuda")
+    try:
+        for r in range(ranks):
+            ctx.fill_synthetic_async(buf.data_ptr(), r * share, share, fx["seed"], s)
+            n = ctx.subtree_device_async(buf.data_ptr(), share, CHUNK, 12, nodes.data_ptr() + 32 * r, s)
+            assert n == 1
+        root = torch.zeros(32, dtype=torch.uint8, device="cuda")
+        ctx.finish_device_async(nodes.data_ptr(), ranks, False, root.data_ptr(), s)
+        torch.cuda.synchronize()
+        got = bytes(nodes.cpu().numpy())
+        assert [got[32 * r:32 * r + 32].hex() for r in range(ranks)] == fx["shard_roots_k12"]
+        assert bytes(root.cpu().numpy()).hex() == fx["root"]
+    finally:
+        del buf
+        torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("length", [8 * GiB + 8, 8 * GiB - 8, 8 * GiB - CHUNK + 4096])
