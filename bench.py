@@ -225,6 +225,9 @@ def main() -> None:
     if world > 1 and (world == 8 or args.in_process) and not args.no_extras and not args.total_gib:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+        # torch keeps freed pinned host blocks cached (configs[4]'s objects: 12.5 GiB per rank); give
+        # them back so the in-process leg's pinned object is not pushed off the GPU's NUMA node
+        torch._C._host_emptyCache()
         dist.barrier(group=wait_group)
         inproc, hung = None, False
         progress("in-process leg (rank 0 over every GPU, in a child process)")
