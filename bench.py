@@ -28,9 +28,9 @@ import time
 from bench_common import (  # noqa: F401
     ROOT, HBM_PEAK_GBS, VALU_SLOT_PEAK, MAX_CLOCK_HZ, ISSUE_CYCLES_ONE_WAVE, SEED, progress,
     start_heartbeat, env_int, host_cpu_facts, cpu_share, PIN_MERKLE, pinning_for, blocks_for, _pcts,
-    PCIE_PEAK_GBS)
+    PCIE_PEAK_GBS, root_fixture)
 from bench_workloads import (  # noqa: F401
-    latency_block, in_process_configs, _summary, EXTRA_ROOF, extras_traffic, extra_roofline, driver_extras,
+    latency_block, in_process_configs, _summary, EXTRA_ROOF, extras_traffic, extra_roofline,
     cpu_fp_baseline, cpu_root_baseline, run_files, run_plumbing, run_upload, run_rs, run_process,
     run_fullprocessing, run_process_upload, run_proofs, run_concurrent, run_batch)
 
@@ -38,21 +38,33 @@ from bench_workloads import (  # noqa: F401
 LEAF_GRID = {"wide": (256, 256), "latency": (64, 128), "pair": (32, 128), "quad": (8, 128)}   # leaves, threads per WG
 
 
-def load_traffic(kind: str, n_leaves: int):
+def load_traffic(kind: str, n_leaves: int, alg_bytes: int = 0):
     """PMC HBM bytes per leaf-kernel launch of this kernel and launch shape, from the committed
     rocprofv3 passes (profiles/k1_traffic.json, made by tools/pmc_traffic.py from the same
-    bench command)."""
+    bench command).  A launch shape that was not profiled (an N > 1 rank's share, say) takes the
+    same kernel's traffic-over-algorithmic ratio at the nearest profiled grid times this launch's
+    algorithmic bytes, and says so in the source."""
     path = os.path.join(ROOT, "profiles", "k1_traffic.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
         d = json.load(f)
     per_wg, threads = LEAF_GRID[kind]
-    key = f"{kind}:{(n_leaves + per_wg - 1) // per_wg * threads}"
+    grid = (n_leaves + per_wg - 1) // per_wg * threads
+    key = f"{kind}:{grid}"
     e = d.get("by_kernel_grid", {}).get(key)
-    if not e:
+    if e:
+        return e["hbm_bytes_per_launch"], f"profiles/k1_traffic.json[{key}] <- " + d.get("source", "")
+    same = [(abs(int(k.split(":")[1]) - grid), k, v) for k, v in d.get("by_kernel_grid", {}).items()
+            if k.split(":")[0] == kind]
+    if not same or not alg_bytes:
         return None, None
-    return e["hbm_bytes_per_launch"], f"profiles/k1_traffic.json[{key}] <- " + d.get("source", "")
+    _, k2, v = min(same)
+    leaves2 = int(k2.split(":")[1]) // threads * per_wg
+    alg2 = (8 << 30) + 32 * leaves2          # every profiled grid hashed the 8 GiB headline object
+    ratio = v["hbm_bytes_per_launch"] / alg2
+    return round(ratio * alg_bytes), (f"profiles/k1_traffic.json[{k2}] ratio {ratio:.5f} x this launch's algorithmic "
+                                      f"bytes ({key} not profiled)")
 
 
 def main() -> None:
@@ -124,6 +136,12 @@ def main() -> None:
                     help="where the full record goes (JSON); default gpurun_out/bench_detail_n<N>.json.  stdout's "
                          "last line is the compact headline, which names this file")
     ap.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling leg")
+    ap.add_argument("--deadline-s", type=float, default=DEADLINE_DEFAULT_S,
+                    help="wall seconds from the job's start within which every leg after the headline must fit: a "
+                         "leg whose estimate exceeds what is left is skipped (named in `problems`); the line is "
+                         "printed again after every leg")
+    ap.add_argument("--fake-legs", type=float, default=0.0, help=argparse.SUPPRESS)
+    ap.add_argument("--fake-line", default="", help=argparse.SUPPRESS)
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--watchdog-check", type=float, default=0.0, help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -136,6 +154,9 @@ def main() -> None:
         return
     if args.watchdog_check:
         watchdog_check(args)
+        return
+    if args.fake_legs:
+        fake_legs(args)
         return
 
     start_heartbeat()
@@ -195,8 +216,11 @@ def main() -> None:
                 dist.barrier(device_ids=[dev_index])
         torch.cuda.synchronize()
 
+    rank0 = rank == 0
+    decide = (lambda mine: mine) if world == 1 else (lambda mine: _bcast_flag(torch, dist, mine, wait_group))
+    detail = args.detail_out or os.path.join(ROOT, "gpurun_out", f"bench_detail_n{1 if args.same_device else world}.json")
     progress("headline: timed steps")
-    out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
+    out = run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier, cpu_leg=not args.no_cpu)
     if isinstance(out.get("parity"), dict):
         out["parity"]["pinned_by"] = PIN_MERKLE
     if world > 1:
@@ -204,50 +228,183 @@ def main() -> None:
         progress("exchange: the all-gather of subtree roots alone")
         out["exchange"] = measure_exchange(plan_shards(out["config"]["object_bytes"], args.chunk, world), torch,
                                            dist, device, gloo, barrier)
-    detail = args.detail_out or os.path.join(ROOT, "gpurun_out", f"bench_detail_n{out['n_gpus']}.json")
-    if world > 1 and not args.total_gib and not args.no_strong:
-        progress("strong-scaling leg: configs[1]'s 8 GiB object over every rank")
-        out["strong_scaling"] = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier,
-                                                   out["value"] / world)
-        progress("strong-scaling leg at 4 KiB chunks (2,097,152 leaves)")
-        out["strong_scaling_4KiB"] = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo,
-                                                        barrier, out["value"] / world, chunk=4096)
-    if world == 1 and rank == 0 and not args.no_extras:
-        out["other_configs"] = driver_extras(args, torch, dist, device, dev_index)
-        progress("latency block")
-        out["latency"] = latency_block(args, torch, dev_index)
-    if ((world == 8 and not args.same_device) or (world > 1 and args.multi_configs)) and not args.no_extras \
-            and not args.total_gib:
-        progress("multi-GPU configs (configs[3], configs[4])")
-        other = multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
-        if rank == 0:
-            out["other_configs"] = other
-    if world > 1 and (world == 8 or args.in_process) and not args.no_extras and not args.total_gib:
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        # torch keeps freed pinned host blocks cached (configs[4]'s objects: 12.5 GiB per rank); give
-        # them back so the in-process leg's pinned object is not pushed off the GPU's NUMA node
-        torch._C._host_emptyCache()
-        dist.barrier(group=wait_group)
-        inproc, hung = None, False
-        progress("in-process leg (rank 0 over every GPU, in a child process)")
-        if rank == 0:
-            leg = ["--workload", "inprocess", "--gpus", "1", "--inproc-gib", str(args.inproc_gib)]
-            if args.same_device:
-                leg += ["--same-device", "--inproc-devices", str(world)]
-            inproc, hung = run_child_leg([sys.executable, os.path.abspath(__file__), *leg], "in_process",
-                                         args.inproc_timeout)
-        flag = torch.tensor([1 if hung else 0], dtype=torch.int64)
-        dist.all_reduce(flag, group=wait_group)           # doubles as the barrier
-        if rank == 0:
-            out.setdefault("other_configs", {})["in_process"] = inproc
-        if int(flag.item()):
-            exit_after_hang(out if rank == 0 else None, detail)
-    if rank == 0:
-        emit(out, detail)
+    legs = Legs(out, detail if rank0 else None, args.deadline_s, job_start_time(), decide)
+    full = not args.no_extras and not args.total_gib
+    if world == 1:
+        if rank0 and not args.no_extras:
+            from bench_workloads import driver_extra_specs, run_driver_extra
+            traffic, tsrc = extras_traffic()
+            specs = driver_extra_specs()
+            legs.plan([name for name, _, _ in specs] + ["latency"])
+            legs.emit()                                       # the headline line, before any extra
+            oc = out.setdefault("other_configs", {})
+            for name, fn, kw in specs:
+                legs.run(name, lambda name=name, fn=fn, kw=kw: oc.__setitem__(
+                    name, run_driver_extra(name, fn, kw, args, torch, dist, device, dev_index, traffic, tsrc)))
+            legs.run("latency", lambda: out.__setitem__("latency", latency_block(args, torch, dev_index)))
+    else:
+        names = []
+        if not args.total_gib and not args.no_strong:
+            names += ["strong_scaling", "strong_scaling_4KiB"]
+        if ((world == 8 and not args.same_device) or args.multi_configs) and full:
+            names += ["configs[3]", "configs[4]"]
+        if (world == 8 or args.in_process) and full:
+            names += ["in_process"]
+        legs.plan(names)
+        legs.emit()                                           # the headline line, before any leg
+        weak_per_gpu = out["value"] / world
+
+        def strong(key, chunk):
+            r = strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu,
+                                   chunk=chunk)
+            out[key] = r
+
+        def in_process():
+            inproc, hung = run_in_process_leg(args, torch, dist, world, rank, wait_group, legs)
+            if rank0:
+                out.setdefault("other_configs", {})["in_process"] = inproc
+            if hung:   # the leg is over (killed): the line says so, then every rank leaves with status 3
+                legs.pending.remove("in_process")
+                out["legs"].update(pending=list(legs.pending))
+                out["legs"]["done"]["in_process"] = inproc.get("watchdog_s") if rank0 else None
+                exit_after_hang(out if rank0 else None, legs.detail)
+
+        runs = {"strong_scaling": lambda: strong("strong_scaling", 32 << 20),
+                "strong_scaling_4KiB": lambda: strong("strong_scaling_4KiB", 4096),
+                "configs[3]": lambda: out.setdefault("other_configs", {}).__setitem__(
+                    "configs[3]", config3_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier)),
+                "configs[4]": lambda: out.setdefault("other_configs", {}).__setitem__(
+                    "configs[4]", config4_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier)),
+                "in_process": in_process}
+        for name in names:
+            legs.run(name, runs[name])
+    if not legs.planned:
+        legs.emit()
     if world > 1:
         barrier()
         dist.destroy_process_group()
+
+
+# Wall seconds each leg after the headline may take at full size (per-rank work, timed on one
+# MI355X: DESIGN.md §8, tools/n8_leg_times.sh), with a margin.  A leg starts only when its
+# estimate fits in what is left of --deadline-s; N = 1's extras and latency block total ~150 s.
+LEG_ESTIMATE_S = {
+    "strong_scaling": 25.0, "strong_scaling_4KiB": 25.0, "configs[3]": 60.0, "configs[4]": 60.0,
+    "in_process": 150.0, "latency": 120.0, "FullProcessing_file": 45.0, "FullProcessing_while_receiving": 60.0,
+}
+LEG_ESTIMATE_DEFAULT_S = 20.0
+DEADLINE_DEFAULT_S = 540.0    # 90 % of the 600 s the driver gave the N = 1 bench (BENCH_r05.json)
+WATCHDOG_MARGIN_S = 30.0      # what the in-process watchdog leaves before the deadline: the kill, the line
+
+
+def _bcast_flag(torch, dist, mine, group):
+    """Rank 0's decision, on every rank (a host-side broadcast over the gloo group)."""
+    t = torch.tensor([1 if mine else 0], dtype=torch.int64)
+    dist.broadcast(t, src=0, group=group)
+    return bool(int(t.item()))
+
+
+def _proc_start_time(pid):
+    """Wall-clock start of process `pid` (Linux /proc), or None."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            st = f.read()
+        ticks = int(st[st.rindex(")") + 2:].split()[19])    # field 22: starttime, clock ticks after boot
+        with open("/proc/uptime") as f:
+            uptime = float(f.read().split()[0])
+        return time.time() - (uptime - ticks / os.sysconf("SC_CLK_TCK"))
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def job_start_time():
+    """When the driver's clock started, as near as this process can tell: DEOSS_BENCH_T0 (bench.py's
+    own self-launch parent sets it), else the earliest start of this process and of the launcher
+    that started it (python -m torch.distributed.run)."""
+    t0 = os.environ.get("DEOSS_BENCH_T0")
+    if t0:
+        try:
+            return float(t0)
+        except ValueError:
+            pass
+    starts = [_proc_start_time(os.getpid()) or time.time()]
+    try:
+        with open(f"/proc/{os.getppid()}/cmdline", "rb") as f:
+            parent = f.read().replace(b"\0", b" ").decode(errors="replace")
+        if "torch.distributed.run" in parent or "torchrun" in parent:
+            starts.append(_proc_start_time(os.getppid()))
+    except OSError:
+        pass
+    return min(t for t in starts if t)
+
+
+class Legs:
+    """The legs after the headline, in order.  Each starts only if its estimate (LEG_ESTIMATE_S)
+    fits in what is left before the deadline -- rank 0 decides, every rank follows (`decide`), so
+    the collectives inside a leg stay matched -- and after the headline and after every leg rank 0
+    prints the whole compact line again.  The last stdout line is therefore always complete and
+    parseable and supersedes the one before: a run the driver kills at its limit still leaves the
+    headline and every leg finished so far (`legs.pending` names the rest).  A skipped leg is named
+    in `problems`; a leg that raised is recorded as that leg's error, never fatal to the line."""
+
+    def __init__(self, out, detail, deadline_s, t0, decide, estimates=None):
+        self.out, self.detail, self.deadline, self.t0, self.decide = out, detail, deadline_s, t0, decide
+        self.estimates = estimates or LEG_ESTIMATE_S
+        self.planned, self.pending = [], []
+        out["legs"] = {"deadline_s": deadline_s, "done": {}, "pending": [], "skipped": {}}
+
+    def left(self):
+        return self.deadline - (time.time() - self.t0)
+
+    def plan(self, names):
+        self.planned, self.pending = list(names), list(names)
+        self.out["legs"]["pending"] = list(names)
+
+    def emit(self):
+        self.out["legs"]["elapsed_s"] = round(time.time() - self.t0, 1)
+        if self.detail is not None:
+            emit(self.out, self.detail)
+
+    def run(self, name, fn):
+        est = self.estimates.get(name, LEG_ESTIMATE_DEFAULT_S)
+        left = self.left()
+        if self.decide(left >= est):
+            progress(f"leg {name}: estimate {est:.1f} s, {left:.1f} s left before the {self.deadline:.1f} s deadline")
+            t = time.time()
+            try:
+                fn()
+            except Exception as e:   # recorded as the leg's error; the line and the later legs go on
+                self.out.setdefault("leg_errors", {})[name] = _short(f"{type(e).__name__}: {e}", 300)
+            self.out["legs"]["done"][name] = round(time.time() - t, 1)
+        else:
+            self.out["legs"]["skipped"][name] = (f"estimated {est:.1f} s > {max(left, 0):.1f} s left before the "
+                                                 f"{self.deadline:.1f} s deadline (--deadline-s)")
+            progress(f"leg {name} skipped: {self.out['legs']['skipped'][name]}")
+        self.pending.remove(name)
+        self.out["legs"]["pending"] = list(self.pending)
+        self.emit()
+
+
+def run_in_process_leg(args, torch, dist, world, rank, wait_group, legs):
+    """N > 1: rank 0 runs the single-process multi-GPU leg in a child process (run_child_leg) while
+    every other rank waits on the host group; its watchdog is --inproc-timeout or what is left
+    before the deadline less WATCHDOG_MARGIN_S, whichever is shorter.  (result, hung) on every rank."""
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    dist.barrier(group=wait_group)
+    inproc, hung = None, False
+    if rank == 0:
+        timeout = max(10.0, min(args.inproc_timeout, legs.left() - WATCHDOG_MARGIN_S))
+        progress(f"in-process leg (rank 0 over every GPU, in a child process; watchdog {timeout:.0f} s)")
+        leg = ["--workload", "inprocess", "--gpus", "1", "--inproc-gib", str(args.inproc_gib)]
+        if args.same_device:
+            leg += ["--same-device", "--inproc-devices", str(world)]
+        inproc, hung = run_child_leg([sys.executable, os.path.abspath(__file__), *leg], "in_process", timeout)
+        if isinstance(inproc, dict):
+            inproc["watchdog_s"] = round(timeout, 1)
+    flag = torch.tensor([1 if hung else 0], dtype=torch.int64)
+    dist.all_reduce(flag, group=wait_group)           # doubles as the barrier
+    return inproc, bool(int(flag.item()))
 
 
 def exit_after_hang(out, detail):
@@ -271,6 +428,31 @@ def watchdog_check(args) -> None:
     if hung:
         exit_after_hang(out, args.detail_out)
     emit(out, args.detail_out)
+
+
+def fake_legs(args) -> None:
+    """Hidden --fake-legs S --fake-line PATH (tests/test_bench_line.py): the N > 1 leg sequence with
+    no torch and no GPU -- the headline line from PATH printed first, then five legs that each
+    sleep S seconds, through the same Legs runner, deadline and per-leg line as the real run -- so a
+    test can kill it mid-leg and read the last stdout line, or give it a short --deadline-s."""
+    with open(args.fake_line) as f:
+        out = json.load(f)
+    out.pop("other_configs", None)
+    names = ["strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process"]
+    legs = Legs(out, args.detail_out, args.deadline_s, job_start_time(), lambda mine: mine,
+                estimates={n: args.fake_legs for n in names})
+    legs.plan(names)
+    legs.emit()
+
+    def leg(name):
+        time.sleep(args.fake_legs)
+        r = {"value": 1.0, "unit": "GiB/s", "ms_per_step": 1.0, "bit_exact": True}
+        if name.startswith("strong"):
+            out[name] = r
+        else:
+            out.setdefault("other_configs", {})[name] = {"bit_exact": True, "devices": 8} if name == "in_process" else r
+    for name in names:
+        legs.run(name, lambda name=name: leg(name))
 
 
 def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu,
@@ -335,8 +517,12 @@ def run_child_leg(cmd, key, timeout_s):
             os.killpg(p.pid, signal.SIGKILL)   # the group this call started (start_new_session), nothing else
         except OSError:
             pass
-        p.wait()
-        return {"error": f"did not finish within {timeout_s} s (watchdog: child process group killed)"}, True
+        try:   # a child stuck in an uninterruptible driver call may never exit: do not wait for it forever
+            p.wait(timeout=30)
+            state = "child process group killed"
+        except subprocess.TimeoutExpired:
+            state = f"child process group killed; pid {p.pid} had not exited 30 s later (left behind)"
+        return {"error": f"did not finish within {timeout_s:.0f} s (watchdog: {state})"}, True
     for ln in reversed(text.splitlines()):
         ln = ln.strip()
         if not ln.startswith("{"):
@@ -365,7 +551,8 @@ def self_launch(n: int, argv) -> int:
         port = sk.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
-    env = dict(os.environ, DEOSS_BENCH_LAUNCHER="bench.py self-launch (child python -m torch.distributed.run)")
+    env = dict(os.environ, DEOSS_BENCH_LAUNCHER="bench.py self-launch (child python -m torch.distributed.run)",
+               DEOSS_BENCH_T0=os.environ.get("DEOSS_BENCH_T0") or str(job_start_time()))
     print(f"bench.py: WORLD_SIZE unset, launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
     return subprocess.call(cmd, env=env)
 
@@ -439,9 +626,10 @@ def launch_info(torch, dist, world, rank, local_rank, dev_index, args):
             "launcher": os.environ.get("DEOSS_BENCH_LAUNCHER", "external (WORLD_SIZE set by the caller's launcher)")}
 
 
-def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
+def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier, cpu_leg=False):
     """One object over all ranks (BASELINE configs[1] at N = 1, the weak-scaling curve, configs[3]
-    with --total-gib 1024): timed steps, roofline, parity legs.  Returns rank 0's line (other ranks
+    with --total-gib 1024): timed steps, roofline, parity legs; with cpu_leg, the CPU baseline
+    (N = 1: over the whole object; N > 1: over rank 0's shard).  Returns rank 0's line (other ranks
     get theirs too, unused).  Buffers are released before returning."""
     from deoss_amd import MerkleContext, plan_shards
     from deoss_amd.sharding import sharded_root
@@ -495,6 +683,19 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
 
     value = total * args.steps / elapsed / (1 << 30)
     read_peak_gbs, read_peak_ms = measure_read_peak(ctx, torch, buf, local_len, sptr, stream)
+    cpu_out = {}
+    if world > 1 and rank == 0 and cpu_leg:
+        # N > 1: the CPU baseline over rank 0's shard (at most 8 GiB of whole leaves), copied back
+        # from HBM before the buffer goes; when that shard is one whole block of 2^k leaves its CPU
+        # root is rank 0's gathered subtree node, checked too
+        sample = min(local_len, max(chunk, (8 << 30) // chunk * chunk))
+        progress(f"CPU baseline over rank 0's shard ({sample} B)")
+        cpu_baseline_over(torch, buf, sample, chunk, cpu_out, total,
+                          f"rank 0's shard of the timed object ({sample} of its {local_len} B)")
+        cpu_root = cpu_out["cpu_baseline"].pop("root")
+        if plan.node_count(0) == 1 and sample == local_len and local_len // chunk == (1 << plan.k) \
+                and local_len % chunk == 0:
+            cpu_out["cpu_baseline"]["shard_root_bit_exact"] = bytes(nodes_dev[:32].cpu().numpy()).hex() == cpu_root
     if world > 1:   # the whole-object buffer is released before the parity legs allocate theirs
         del buf
         torch.cuda.empty_cache()
@@ -506,7 +707,7 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
     n_local = (local_len + chunk - 1) // chunk
     kind = ctx.leaf_kernel_for(n_local)
     vpb, spb = kernel_counts(kind)
-    traffic, traffic_src = load_traffic(kind, n_local)
+    traffic, traffic_src = load_traffic(kind, n_local, k1_bytes)
     kernel_name = {"wide": "leaf_kernel (K1, one lane per leaf)",
                    "latency": "leaf_kernel_lat (K1L, producer/consumer waves)",
                    "pair": "leaf_kernel_pair (K1P, producer/consumer, rounds on lane pairs)",
@@ -592,88 +793,76 @@ def run_object(args, torch, dist, world, rank, device, dev_index, gloo, barrier)
         out["note"] = "rehearsal: every rank on cuda:0 of one GPU; not a multi-GPU result"
     if world == 1 and rank == 0:
         extras(args, ctx, torch, buf, local_len, chunk, root_hex, out, sptr)
-        par = out.get("cpu_baseline", {}).get("parallel")
-        est = out.get("cpu_baseline", {}).get("all_physical_cores_estimate", {})
-        if par and par.get("value"):
-            out["vs_cpu_share"] = round(value / par["value"], 4)
-        if est.get("value"):
-            # BASELINE.md publishes no reference number, so vs_baseline stays null (the contract);
-            # the CPU comparisons are their own fields: the measured job share, and the whole
-            # host's CPU (the per-thread rate at the share scaled to every physical core)
-            out["vs_cpu_all_cores"] = round(value / est["value"], 4)
-            out["vs_cpu_basis"] = (f"GPU value / the CPU restatement's rate on the job's {par['cores']} threads "
-                                   f"(vs_cpu_share, measured) and on all {est['cores']} physical cores of this "
-                                   "host (vs_cpu_all_cores, estimated from that run); same object, same run")
+    out.update(cpu_out)
+    cb = out.get("cpu_baseline") or {}
+    par, est = cb.get("parallel") or {}, cb.get("all_physical_cores_estimate") or {}
+    if rank == 0 and par.get("value") and est.get("value"):
+        # BASELINE.md publishes no reference number, so vs_baseline stays null (the contract); the
+        # CPU comparisons are their own fields: the job's CPU share (measured; at N > 1 the per-GPU
+        # share's rate times N) and every physical core of the host (estimated from that run)
+        out["vs_cpu_share"] = round(value / (par["value"] * (world if not args.same_device else 1)), 4)
+        out["vs_cpu_all_cores"] = round(value / est["value"], 4)
+        out["vs_cpu_basis"] = (f"GPU value / the CPU restatement on the job's {par['cores']} threads"
+                               + (f" x {world} GPUs' shares" if world > 1 and not args.same_device else "")
+                               + f" (vs_cpu_share) and on all {est['cores']} physical cores of this host "
+                               "(vs_cpu_all_cores, estimated from that run); same bytes, same run")
     if world > 1 and not args.no_verify:
         out["parity"] = multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, chunk,
                                           root_hex, barrier, gloo)
-        cpu = out["parity"].get("cpu_root_gibs")
-        if rank == 0 and cpu:
-            out["vs_cpu_threads"] = round(value / cpu, 4)
-            out["vs_cpu_basis"] = (f"GPU value / the {out['parity']['cpu_threads']}-thread CPU restatement over "
-                                   "the same synthetic object (regenerated leaf by leaf), same run")
     del ctx
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out
 
 
-def multi_gpu_configs(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
-    """N = 8: BASELINE configs[3] (one 1 TiB object, 128 GiB and 4,096 leaves per GPU, sharded
-    root + both parity legs) and configs[4] (100,000 x 1 MiB objects from pinned host memory,
-    12,500 per GPU, replicas), measured in the same run as the weak-scaling line so the driver's
-    8-GPU run records them.  Every rank takes part in both (collectives); configs[3] runs only if
-    every rank has the HBM for it, agreed by one all-reduce before anything is allocated."""
+def config3_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
+    """N = 8: BASELINE configs[3], one 1 TiB object (128 GiB and 4,096 leaves per GPU): the sharded
+    root timed, checked against a single-GPU root of its 64 GiB prefix and against the committed
+    full-size fixture (tests/golden/config3_root.json), which replaces re-hashing 1 TiB on the host
+    CPU.  Runs only if every rank has the HBM for it, agreed by one all-reduce before anything is
+    allocated; an error every rank meets (DM_ERR_NOMEM, say) costs this entry, not the line."""
     import copy
-    res = {}
+    t0 = time.perf_counter()
     need = int(args.cfg3_total_gib * (1 << 30)) // world + (8 << 30)
     free, _ = torch.cuda.mem_get_info(device)
     ok = torch.tensor([1 if free >= need else 0], dtype=torch.int64, device="cpu" if gloo else device)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    t0 = time.perf_counter()
-    if int(ok.item()):
-        ns = copy.copy(args)
-        ns.total_gib, ns.steps, ns.warmup, ns.no_extras = args.cfg3_total_gib, 3, 1, True
-        try:   # an error every rank meets (the library's DM_ERR_NOMEM, say) costs this entry, not the line
-            r3 = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
-            res["configs[3]"] = _summary(r3)
-            res["configs[3]"]["pinned_by"] = PIN_MERKLE
-            fx = config3_fixture(ns.total_gib, args.chunk)
-            if fx and rank == 0:   # the full-size fixture the one-GPU test reproduces shard by shard
-                res["configs[3]"]["fixture_root"] = fx["root"]
-                res["configs[3]"]["fixture_bit_exact"] = r3.get("root") == fx["root"]
-        except Exception as e:
-            res["configs[3]"] = {"error": f"{type(e).__name__}: {e}"}
-            torch.cuda.empty_cache()
-    else:
-        res["configs[3]"] = {"skipped": f"a rank has less than {need} B of free HBM"}
-    res["configs[3]"]["wall_s"] = round(time.perf_counter() - t0, 2)
-    barrier()
-    t0 = time.perf_counter()
+    if not int(ok.item()):
+        return {"skipped": f"a rank has less than {need} B of free HBM", "wall_s": round(time.perf_counter() - t0, 2)}
     ns = copy.copy(args)
-    ns.workload, ns.total_objects, ns.object_mib, ns.steps, ns.warmup = "stream", args.cfg4_objects, 1.0, 2, 1
+    ns.total_gib, ns.steps, ns.warmup, ns.no_extras = args.cfg3_total_gib, 3, 1, True
     try:
-        res["configs[4]"] = _summary(run_batch(ns, torch, dist, world, rank, device, dev_index, gloo))
-        res["configs[4]"]["pinned_by"] = PIN_MERKLE
+        r3 = run_object(ns, torch, dist, world, rank, device, dev_index, gloo, barrier)
+        res = _summary(r3)
+        res["pinned_by"] = PIN_MERKLE
+        fx = root_fixture(int(ns.total_gib * (1 << 30)), args.chunk, SEED)
+        if fx and rank == 0:
+            res["fixture_root"] = fx["root"]
+            res["fixture_bit_exact"] = r3.get("root") == fx["root"]
     except Exception as e:
-        res["configs[4]"] = {"error": f"{type(e).__name__}: {e}"}
-    res["configs[4]"]["wall_s"] = round(time.perf_counter() - t0, 2)
-    torch.cuda.empty_cache()
+        res = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.empty_cache()
+    res["wall_s"] = round(time.perf_counter() - t0, 2)
     barrier()
     return res
 
 
-def config3_fixture(total_gib, chunk):
-    """tests/golden/config3_root.json (the 1 TiB configs[3] root at bench.py's seed, from the oracle
-    leaf by leaf) when the run hashes exactly that object, else None."""
-    path = os.path.join(ROOT, "tests", "golden", "config3_root.json")
+def config4_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier):
+    """N = 8: BASELINE configs[4], 100,000 x 1 MiB objects from pinned host memory, 12,500 per GPU
+    (replicas, no exchange); every root of every rank checked against the CPU restatement."""
+    import copy
+    t0 = time.perf_counter()
+    ns = copy.copy(args)
+    ns.workload, ns.total_objects, ns.object_mib, ns.steps, ns.warmup = "stream", args.cfg4_objects, 1.0, 2, 1
     try:
-        with open(path) as f:
-            fx = json.load(f)
-    except (OSError, ValueError):
-        return None
-    ok = int(total_gib * (1 << 30)) == fx.get("len") and chunk == fx.get("chunk") and fx.get("seed") == SEED
-    return fx if ok else None
+        res = _summary(run_batch(ns, torch, dist, world, rank, device, dev_index, gloo))
+        res["pinned_by"] = PIN_MERKLE
+    except Exception as e:
+        res = {"error": f"{type(e).__name__}: {e}"}
+    res["wall_s"] = round(time.perf_counter() - t0, 2)
+    torch.cuda.empty_cache()
+    barrier()
+    return res
 
 
 LINE_MAX_BYTES = 6144   # the last stdout line; the driver lost r04's 28 KB line (VERDICT r4 item 1)
@@ -737,6 +926,24 @@ def _in_process_line(r):
     return e
 
 
+def route_constants(out):
+    """What this N > 1 line measured for the routing model's two estimated constants (dm_plan::route,
+    DESIGN.md §7), as the environment variables dm_create reads in their place: DEOSS_ALLGATHER_US
+    (the all-gather timed alone, `exchange.avg_us`) and DEOSS_HOST_BYTES_PER_S (the node's aggregate
+    zero-copy host read rate, `in_process.host_feed.all_GBps`).  Only from real GPUs over RCCL: a
+    one-GPU rehearsal's numbers are not a node's."""
+    ex = out.get("exchange") or {}
+    if out.get("same_device") or "nccl" not in str(ex.get("backend", "")):
+        return None
+    rc = {}
+    if ex.get("avg_us"):
+        rc["DEOSS_ALLGATHER_US"] = round(float(ex["avg_us"]), 1)
+    hf = ((out.get("other_configs") or {}).get("in_process") or {}).get("host_feed") or {}
+    if isinstance(hf, dict) and hf.get("all_GBps") and hf.get("consistent"):
+        rc["DEOSS_HOST_BYTES_PER_S"] = int(float(hf["all_GBps"]) * 1e9)
+    return rc or None
+
+
 def compact_line(out, detail_path=None):
     """Rank 0's last stdout line, at most LINE_MAX_BYTES: the headline and its evidence (roofline,
     CPU baseline, parity, host-buffer rate, launch at N > 1) plus one short entry per extra.  The
@@ -780,6 +987,11 @@ def compact_line(out, detail_path=None):
         if host.get("model"):
             c["host"] = _short(host["model"], 60)
         line["cpu_baseline"] = c
+        for k in ("parallel_roots_agree", "shard_root_bit_exact"):
+            if k in cb:
+                c[k] = cb[k]
+                if cb[k] is False:
+                    problems.append(f"cpu_baseline.{k}")
     for k in ("vs_cpu_share", "vs_cpu_all_cores", "vs_cpu_threads"):
         if k in out:
             line[k] = out[k]
@@ -787,8 +999,11 @@ def compact_line(out, detail_path=None):
         line["vs_cpu_basis"] = _short(out["vs_cpu_basis"], 220)
     par = out.get("parity")
     if isinstance(par, dict):
-        p = {k: par[k] for k in ("bit_exact", "prefix_bit_exact", "cpu_bit_exact", "gpu_root", "cpu_root",
-                                 "sharded_root", "prefix_bytes", "cpu_threads", "cpu_root_gibs") if k in par}
+        p = {k: par[k] for k in ("bit_exact", "prefix_bit_exact", "prefix_fixture_bit_exact", "cpu_bit_exact",
+                                 "gpu_root", "cpu_root", "sharded_root", "prefix_bytes", "cpu_threads",
+                                 "cpu_root_gibs", "single_gpu_ms") if k in par}
+        if par.get("cpu_root_source"):
+            p["cpu_root_source"] = _short(par["cpu_root_source"], 90)
         line["parity"] = p
         if par.get("bit_exact") is not True:
             problems.append("parity")
@@ -812,6 +1027,9 @@ def compact_line(out, detail_path=None):
     ex = out.get("exchange")
     if isinstance(ex, dict):
         line["exchange"] = {k: ex.get(k) for k in ("backend", "bytes_per_rank", "ranks", "avg_us")}
+        rc = route_constants(out)
+        if rc:
+            line["route_constants"] = rc
     for k in ("same_device", "note", "ranks"):
         if k in out:
             line[k] = out[k]
@@ -845,6 +1063,16 @@ def compact_line(out, detail_path=None):
         line["latency"] = lt
         if lat.get("bit_exact") is not True:
             problems.append("latency")
+    lg = out.get("legs")
+    if isinstance(lg, dict):
+        line["legs"] = {k: lg[k] for k in ("deadline_s", "elapsed_s", "done", "pending") if k in lg}
+        if lg.get("skipped"):
+            line["legs"]["skipped"] = {k: _short(v, 120) for k, v in lg["skipped"].items()}
+            problems += [f"skipped:{k}" for k in lg["skipped"]]
+        line["complete"] = not lg.get("pending")
+    for k, v in (out.get("leg_errors") or {}).items():
+        line.setdefault("leg_errors", {})[k] = _short(v, 160)
+        problems.append(f"error:{k}")
     line["ok"] = not problems
     if problems:
         line["problems"] = problems
@@ -905,8 +1133,10 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
     """Untimed N>1 checks that fit any object size:
     1. prefix: the sharded path over a prefix of <= --prefix-gib (the whole object when it fits)
        vs a single-GPU root of the same prefix on rank 0;
-    2. CPU: the oracle's N-thread root of the WHOLE object, its bytes regenerated leaf by leaf on
-       the host (no whole-object buffer anywhere: 1 TiB fits)."""
+    2. the whole object's root vs its committed full-size fixture (root_fixture: made leaf by leaf
+       by the C oracle; the prefix too when one is committed) -- no host re-hash of up to 1 TiB
+       inside the driver's time limit.  Without a fixture (reduced rehearsal sizes): the oracle's
+       N-thread root of the WHOLE object, its bytes regenerated leaf by leaf on the host."""
     from deoss_amd import plan_shards
     from deoss_amd.sharding import parity_prefix, sharded_root
     res = {"sharded_root": root_hex}
@@ -955,7 +1185,16 @@ def multi_rank_parity(args, torch, dist, ctx, world, rank, device, sptr, total, 
         res.update({"prefix_bytes": prefix, "prefix_sharded_root": sharded_prefix, "prefix_single_gpu_root": single,
                     "prefix_bit_exact": single == sharded_prefix})
         ok = single == sharded_prefix
-        if not args.no_cpu:
+        pfx = root_fixture(prefix, chunk, SEED) if prefix != total else None
+        if pfx:
+            res.update({"prefix_fixture_root": pfx["root"], "prefix_fixture_bit_exact": single == pfx["root"]})
+            ok = ok and single == pfx["root"]
+        fx = root_fixture(total, chunk, SEED)
+        if fx:
+            res.update({"cpu_root": fx["root"], "cpu_root_source": f"{fx['file']} [{fx['name']}] (oracle, leaf by leaf)",
+                        "cpu_bit_exact": fx["root"] == root_hex})
+            ok = ok and fx["root"] == root_hex
+        elif not args.no_cpu:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             from oracle import Oracle
             threads = max(1, min(os.cpu_count() or 1, cpu_share() * (1 if args.same_device else world)))   # job CPU share
@@ -1009,6 +1248,64 @@ def concurrent_callers(ctx, host, length, chunk, root_hex, one_s, dev_index):
     return res
 
 
+def cpu_baseline_block(orc, host_ptr, length, chunk, total, out, what):
+    """out["cpu_baseline"]: the faithful serial restatement of common/hashtree (1 core, SHA-NI when
+    present: stands in for Go crypto/sha256) over `length` bytes of pinned host memory, the same
+    bytes on the job's CPU share and on half of it, and the rate every physical core of this host
+    would reach on the whole `total`-byte object.  Returns (serial root, the parallel roots agree)."""
+    facts = host_cpu_facts()
+    t0 = time.perf_counter()
+    _, cpu_root = orc.root_buffer_ptr(host_ptr, length, chunk, nthreads=1)
+    t1 = time.perf_counter()
+    nthr = facts["share"]
+    _, cpu_root_p = orc.root_buffer_ptr(host_ptr, length, chunk, nthreads=nthr)
+    t2 = time.perf_counter()
+    half = max(1, nthr // 2)
+    _, cpu_root_h = orc.root_buffer_ptr(host_ptr, length, chunk, nthreads=half)
+    t3 = time.perf_counter()
+    serial = length / (t1 - t0) / (1 << 30)
+    par = length / (t2 - t1) / (1 << 30)
+    # Every leaf is one serial chain on one core, so P physical cores hash the object's n leaves in
+    # ceil(n / P) rounds of one chain, each as long as one round measured at the share.
+    n_sample = (length + chunk - 1) // chunk
+    n_total = (total + chunk - 1) // chunk
+    P = facts["physical_cores"] or facts["logical_cpus"]
+    chain_s = (t2 - t1) / -(-n_sample // nthr)
+    rounds_all = -(-n_total // P)
+    est_all = total / (rounds_all * chain_s) / (1 << 30) if chain_s > 0 else None
+    out["cpu_baseline"] = {
+        "value": round(serial, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{what}, chunk {chunk}, serial leaves then tree (oracle/merkle_oracle.c, SHA-256 backend "
+                  f"{orc.backend()}; stands in for Go crypto/sha256)",
+        "host": facts, "root": cpu_root.hex(),
+        "parallel": {"value": round(par, 4), "cores": nthr,
+                     "scaling": {"1": round(serial, 4), str(half): round(length / (t3 - t2) / (1 << 30), 4),
+                                 str(nthr): round(par, 4)},
+                     "note": "leaves across the job's CPU share (the GPU box allots 16 CPUs per GPU; "
+                             "os.cpu_count() there is the whole machine)"},
+        "all_physical_cores_estimate": {
+            "value": round(est_all, 4) if est_all else None, "cores": P,
+            "method": f"the whole {total} B object's {n_total} leaves in ceil({n_total}/{P}) = {rounds_all} rounds "
+                      f"of one chain, a chain as long as one round measured at the share ({chain_s:.3f} s); "
+                      "estimated, not run: the box's job limits forbid using every core"},
+    }
+    return cpu_root, cpu_root_h == cpu_root_p == cpu_root
+
+
+def cpu_baseline_over(torch, buf, length, chunk, out, total, what):
+    """cpu_baseline_block over the first `length` bytes of device buffer `buf`, copied to pinned
+    host memory first (N > 1: rank 0's shard)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import Oracle   # CPU baseline / checker only
+    host = torch.empty(length, dtype=torch.uint8, pin_memory=True)
+    host.copy_(buf[:length])
+    torch.cuda.synchronize()
+    root, ok = cpu_baseline_block(Oracle(), host.data_ptr(), length, chunk, total, out, what)
+    out["cpu_baseline"]["parallel_roots_agree"] = ok
+    del host
+    return root
+
+
 def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
@@ -1022,46 +1319,11 @@ def extras(args, ctx, torch, buf, length, chunk, root_hex, out, sptr):
         torch.cuda.synchronize()
     if not args.no_cpu:
         progress("CPU baseline over the headline object")
-        # faithful serial restatement of common/hashtree over the same 8 GiB (1 core, SHA-NI when present)
-        facts = host_cpu_facts()
-        t0 = time.perf_counter()
-        _, cpu_root = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=1)
-        t1 = time.perf_counter()
-        nthr = facts["share"]
-        _, cpu_root_p = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=nthr)
-        t2 = time.perf_counter()
-        half = max(1, nthr // 2)
-        _, cpu_root_h = orc.root_buffer_ptr(host.data_ptr(), length, chunk, nthreads=half)
-        t3 = time.perf_counter()
-        serial = length / (t1 - t0) / (1 << 30)
-        par = length / (t2 - t1) / (1 << 30)
-        # Every leaf is one serial chain on one core, so a host with P physical cores hashes the
-        # n leaves in ceil(n / P) rounds of one chain (the per-thread rate measured at the share).
-        n_leaves = (length + chunk - 1) // chunk
-        P = facts["physical_cores"] or facts["logical_cpus"]
-        per_thread = par / nthr
-        rounds_share = -(-n_leaves // nthr)
-        rounds_all = -(-n_leaves // P)
-        est_all = per_thread * nthr * rounds_share / rounds_all if rounds_all else None
-        out["cpu_baseline"] = {
-            "value": round(serial, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-            "sample": f"the full {length} B object of the timed workload, chunk {chunk}, serial leaves then tree "
-                      f"(oracle/merkle_oracle.c, SHA-256 backend {orc.backend()}; stands in for Go crypto/sha256)",
-            "host": facts,
-            "parallel": {"value": round(par, 4), "cores": nthr,
-                         "scaling": {"1": round(serial, 4), str(half): round(length / (t3 - t2) / (1 << 30), 4),
-                                     str(nthr): round(par, 4)},
-                         "note": "leaves across the job's CPU share (the GPU box allots 16 CPUs per GPU; "
-                                 "os.cpu_count() there is the whole machine)"},
-            "all_physical_cores_estimate": {
-                "value": round(est_all, 4) if est_all else None, "cores": P,
-                "method": f"per-thread rate at the share x min(P, leaves): {n_leaves} leaves in "
-                          f"ceil({n_leaves}/{P}) = {rounds_all} rounds of one chain instead of {rounds_share}; "
-                          "measured, not run: the box's job limits forbid using every core"},
-        }
-        cpu_root_p = cpu_root_p if cpu_root_h == cpu_root_p else b"mismatch"
+        cpu_root, cpu_ok = cpu_baseline_block(orc, host.data_ptr(), length, chunk, length, out,
+                                              f"the full {length} B object of the timed workload")
+        out["cpu_baseline"].pop("root")
         out["parity"] = {"gpu_root": root_hex, "cpu_root": cpu_root.hex(),
-                         "bit_exact": cpu_root.hex() == root_hex and cpu_root_p == cpu_root}
+                         "bit_exact": cpu_root.hex() == root_hex and cpu_ok}
     if do_e2e and host is not None:
         progress("host-buffer end to end")
         # host pinned buffer -> H2D (overlapped) -> root -> 32 B back (the upload-handler path)

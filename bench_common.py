@@ -18,9 +18,11 @@ PHASE = ["start"]   # what the run is doing now (stderr progress lines, heartbea
 
 
 def progress(phase: str) -> None:
-    """One stderr line per phase (stdout carries only the JSON line), and the heartbeat's label."""
+    """One stderr line per phase (stdout carries only the JSON line), and the heartbeat's label.
+    Only rank 0 prints (the other ranks run the same phases)."""
     PHASE[0] = phase
-    print(f"[bench] {time.strftime('%H:%M:%S')} {phase}", file=sys.stderr, flush=True)
+    if os.environ.get("RANK", "0") in ("", "0"):
+        print(f"[bench] {time.strftime('%H:%M:%S')} {phase}", file=sys.stderr, flush=True)
 
 
 def start_heartbeat(period_s: float = 50.0) -> None:
@@ -31,7 +33,8 @@ def start_heartbeat(period_s: float = 50.0) -> None:
     def beat():
         while True:
             time.sleep(period_s)
-            print(f"[bench] {time.strftime('%H:%M:%S')} ... {PHASE[0]}", file=sys.stderr, flush=True)
+            if os.environ.get("RANK", "0") in ("", "0"):
+                print(f"[bench] {time.strftime('%H:%M:%S')} ... {PHASE[0]}", file=sys.stderr, flush=True)
 
     threading.Thread(target=beat, daemon=True).start()
 
@@ -160,3 +163,35 @@ PCIE_PEAK_GBS = 64.0   # PCIe 5.0 x16, one direction, raw (about 55 GB/s measure
 def golden_case(name):
     with open(os.path.join(ROOT, "tests", "golden", "merkle_golden.json")) as f:
         return next(c for c in json.load(f)["cases"] if c["name"] == name)
+
+
+def root_fixture(length, chunk, seed=SEED):
+    """The committed full-size root of the splitmix64 object [0, length) of stream `seed` at `chunk`
+    -- tests/golden/merkle_golden.json (configs[0], configs[1]), config3_root.json (configs[3],
+    1 TiB) and scale_roots.json (the N > 1 weak objects, the 4 KiB strong leg), each made leaf by
+    leaf by the C oracle -- as {"root", "name", "file"}, or None when none is committed.  The N > 1
+    legs check their roots against it instead of re-hashing up to 1 TiB on the host inside the
+    driver's time limit."""
+    gold = os.path.join(ROOT, "tests", "golden")
+    found = []
+    try:
+        with open(os.path.join(gold, "merkle_golden.json")) as f:
+            found += [(c, "merkle_golden.json") for c in json.load(f)["cases"]
+                      if c.get("kind") == "buffer" and c.get("full_size")]
+    except (OSError, ValueError, KeyError):
+        pass
+    try:
+        with open(os.path.join(gold, "config3_root.json")) as f:
+            found.append((json.load(f), "config3_root.json"))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open(os.path.join(gold, "scale_roots.json")) as f:
+            d = json.load(f)
+        found += [(dict(r, seed=d["seed"]), "scale_roots.json") for r in d["roots"]]
+    except (OSError, ValueError, KeyError):
+        pass
+    for c, fname in found:
+        if c.get("len") == length and c.get("chunk") == chunk and c.get("seed") == seed:
+            return {"root": c["root"], "name": c.get("name"), "file": f"tests/golden/{fname}"}
+    return None

@@ -2,7 +2,7 @@
 BASELINE configs[0], [2] and [4] as batches, files through NewHashTree, the streamed upload,
 Reed-Solomon, FullProcessing (in HBM, from a file, while receiving), proofs, concurrent callers,
 the per-request latency block and the single-process multi-GPU leg; plus the N = 1 line's
-`driver_extras` orchestration and the step-level roofline each extra carries.  Every result is
+`driver_extra_specs` / `run_driver_extra` and the step-level roofline each extra carries.  Every result is
 checked against the CPU oracle (test infrastructure, outside the timed regions)."""
 from __future__ import annotations
 
@@ -515,7 +515,7 @@ def _summary(r):
 
 # Step-level roofline of each N = 1 extra: (profiles/extras_traffic.json key, bound, algorithmic
 # bytes one step must move on the bound's link, what they are, the bytes this design's own kernels
-# must move on the memory side per step, what those are).  Sizes are driver_extras()'s.  The PMC
+# must move on the memory side per step, what those are).  Sizes are driver_extra_specs()'s.  The PMC
 # traffic of the kernels is compared with the design bytes; the blit copies (__amd_rocclr_*) are
 # reported apart, since their counter widths across PCIe are uncalibrated.
 EXTRA_ROOF = {
@@ -592,12 +592,11 @@ def extra_roofline(name, r, traffic, src):
     r["roofline"] = roof
 
 
-def driver_extras(args, torch, dist, device, dev_index):
-    """N = 1 only: the other BASELINE configs and entry points, measured in the same run as the
-    headline so the round's driver records them (each is also its own --workload).  A failing
-    extra is reported as an error field; it never fails the headline."""
-    import copy
-    specs = [
+def driver_extra_specs():
+    """N = 1 only: the other BASELINE configs and entry points measured in the same run as the
+    headline so the round's driver records them (each is also its own --workload), as
+    (name, runner, argument overrides), in the order bench.py runs them (one leg each)."""
+    return [
         ("configs[0]", run_plumbing, dict(workload="plumbing", steps=2, warmup=1)),
         ("configs[2]", run_batch, dict(workload="batch", objects=4096, object_mib=4.0, steps=3, warmup=1)),
         ("configs[4]_per_gpu_share", run_batch, dict(workload="stream", objects=12500, object_mib=1.0, steps=2,
@@ -612,25 +611,28 @@ def driver_extras(args, torch, dist, device, dev_index):
         ("FullProcessing_while_receiving", run_process_upload, dict(workload="process_upload", object_gib=2.0,
                                                                     piece_kib=1024, steps=2, warmup=1)),
     ]
-    res = {}
-    traffic, tsrc = extras_traffic()
-    for name, fn, kw in specs:
-        progress(f"extra {name}")
-        ns = copy.copy(args)
-        ns.__dict__.update(kw)
-        t0 = time.perf_counter()
-        try:
-            r = _summary(fn(ns, torch, dist, 1, 0, device, dev_index, False))
-            r["pinned_by"] = pinning_for(ns.workload, getattr(ns, "mode", "root"))
-            extra_roofline(name, r, traffic, tsrc)
-        except Exception as e:   # reported, never fatal to the headline line
-            r = {"error": f"{type(e).__name__}: {e}"}
-        r["wall_s"] = round(time.perf_counter() - t0, 2)
-        res[name] = r
-        gc.collect()   # the workload's contexts and buffers go now, not during the next one's timing
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-    return res
+
+
+def run_driver_extra(name, fn, kw, args, torch, dist, device, dev_index, traffic, tsrc):
+    """One extra of driver_extra_specs() on this GPU: its summary with the step-level roofline
+    (extra_roofline) and its wall time.  A failing extra is reported as an error field; it never
+    fails the headline."""
+    import copy
+    progress(f"extra {name}")
+    ns = copy.copy(args)
+    ns.__dict__.update(kw)
+    t0 = time.perf_counter()
+    try:
+        r = _summary(fn(ns, torch, dist, 1, 0, device, dev_index, False))
+        r["pinned_by"] = pinning_for(ns.workload, getattr(ns, "mode", "root"))
+        extra_roofline(name, r, traffic, tsrc)
+    except Exception as e:   # reported, never fatal to the headline line
+        r = {"error": f"{type(e).__name__}: {e}"}
+    r["wall_s"] = round(time.perf_counter() - t0, 2)
+    gc.collect()   # the workload's contexts and buffers go now, not during the next one's timing
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return r
 
 
 def cpu_fp_baseline(orc, addr, length, seg, what, serial_segs=2, par_segs=64):

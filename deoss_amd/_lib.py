@@ -44,7 +44,7 @@ EXPORTS = (
     "dm_verify_object_device_async",
     "dm_batcher_create", "dm_batcher_destroy", "dm_batcher_root", "dm_batcher_process", "dm_batcher_stats",
     "dm_batcher_last_error",
-    "dm_plan_shards", "dm_plan_route", "dm_pstream_stats", "dm_exchange_timing", "dm_last_call_devices",
+    "dm_plan_shards", "dm_plan_route", "dm_route_constants", "dm_pstream_stats", "dm_exchange_timing", "dm_last_call_devices",
 )
 
 
@@ -136,6 +136,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "dm_last_call_devices": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32), i32, ctypes.POINTER(i32)], i32),
         "dm_plan_shards": ([u64, i32, ctypes.POINTER(u32), pu64, pu64, pu64], i32),
         "dm_plan_route": ([u64, u64, u64, i32, i32, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_double)], i32),
+        "dm_route_constants": ([vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)], i32),
     }
     for name, (args, res) in sigs.items():
         f = getattr(L, name)

@@ -277,7 +277,13 @@ struct Reaper {
         }
     }
     // Block until everything queued so far has been freed (an allocation that failed for lack of
-    // memory retries after this).  The frees wait for the devices' queued work, never for a lock.
+    // memory retries after this).  Each free goes through dev_release / host_release: it takes that
+    // device's allocation mutex (or the host one) and holds it across a hipFree / hipHostFree that
+    // waits for the device's queued work, so meanwhile every allocation on that device (for a host
+    // free: every pinned allocation of the process) waits too.  Deadlock-free because those mutexes
+    // are leaves: no code holds a device or host allocation mutex while calling reaper_drain or
+    // taking any other library lock (DevBuf::ensure drains the reaper between two dev_alloc calls,
+    // holding neither mutex).
     void drain() {
         std::unique_lock<std::mutex> lk(mu);
         idle.wait(lk, [&] { return q.empty() && active == 0; });
@@ -371,6 +377,14 @@ struct dm_ctx {
     // Test hook (env DEOSS_FORCE_SHARDED=1 at dm_create): run host-memory objects through the
     // multi-device path (partition, RCCL all-gather, compaction, finish) even with one device.
     bool force_sharded = false;
+    // The routing model's all-gather and host-bandwidth terms: estimates, or the values an N = 8
+    // bench line measured, from DEOSS_ALLGATHER_US / DEOSS_HOST_BYTES_PER_S at dm_create.
+    dm_plan::RouteConstants route_k;
+    // Test hook (env DEOSS_TEST_RCCL_INIT_FAIL=1 at dm_create of a multi-device context that is not
+    // forced sharded): comms_for fails the way a failing ncclCommInitAll does, just before calling
+    // it, so dm_create's degraded path runs end to end on one GPU (virtual devices otherwise never
+    // build communicators).
+    bool fail_comm_init = false;
     // Test hook (env DEOSS_VIRTUAL_DEVICES=N at dm_create): N context devices on the first GPU, each
     // with its own streams, scratch and lock, so routing, range locks, multi_root's partition and
     // compaction and the batch split run with G = N on a one-GPU box.  RCCL rejects duplicate
@@ -1294,6 +1308,8 @@ int comms_for(dm_ctx* c, int G, std::vector<ncclComm_t>** out) {
         std::vector<int> ids(G);
         for (int g = 0; g < G; g++) ids[g] = c->devs[g].id;
         std::vector<ncclComm_t> cm(G);
+        if (c->fail_comm_init)
+            return fail(c, DM_ERR_RCCL, "ncclCommInitAll over %d GPUs: injected failure (DEOSS_TEST_RCCL_INIT_FAIL=1)", G);
         NCCL_TRY(ncclCommInitAll(cm.data(), G, ids.data()));
         it = c->comms.emplace(G, std::move(cm)).first;
     }
@@ -1447,7 +1463,8 @@ int route_call(dm_ctx* c, uint64_t n, uint64_t bytes, uint64_t leaf_max, int src
     const int G = c->nphys;   // GPUs; a call never shards over lanes of one GPU
     if (c->force_sharded) return n >= 2 * (uint64_t)G ? G : 1;
     if (G <= 1 || (!c->shard_ok && !by_objects)) return 1;
-    return dm_plan::route(n, bytes, leaf_max, src, G, c->devs[0].cus, c->leaf_mode.load(), ctx_load(c), by_objects);
+    return dm_plan::route(n, bytes, leaf_max, src, G, c->devs[0].cus, c->leaf_mode.load(), ctx_load(c), by_objects,
+                          nullptr, c->route_k);
 }
 
 // Whether a call of n leaves routed to G devices takes the multi-device path (with
@@ -1603,26 +1620,47 @@ void keep_claim(int dev, int64_t delta) {
     v = delta < 0 && (uint64_t)(-delta) > v ? 0 : v + delta;
 }
 
-// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else sized from the
-// context's first GPU's HBM and claims (a multi-GPU context uses the same count on every GPU).  Every lane runs on a hardware queue of its own (init_device), so L lanes
+// Call lanes per GPU when the caller does not say (dm_create): DEOSS_LANES, else sized from every
+// GPU of the context's HBM and claims (the same count on each).  Every lane runs on a hardware
+// queue of its own (init_device), so L lanes
 // overlap L large calls (measured: 2 lanes 2x, 4 lanes 4x for pageable 2 GiB objects, PCIe-bound
 // at 4 for pinned 8 GiB ones; tools/lanes_probe.py, profiles/r03/LOGS.md#r03w_lanes.log).  What a lane
-// costs while idle is the object buffer it keeps between calls, at most kLaneKeepBytes (16 GiB),
+// costs while idle is the object buffer it keeps between calls, at most lane_keep_bytes() (16 GiB),
 // so the default is as many lanes (1 to 4) as keep (a) at most half of the free HBM idle and (b),
 // together with every other live context's claim on this GPU, at most half of the GPU's HBM:
 // 4 for the first two default contexts on an MI355X (288 GB), then 1.
-int default_lanes(int dev) {
+// The object buffer each lane of a context created now keeps between calls: DEOSS_LANE_KEEP_BYTES
+// (a test hook; a whole non-negative number of bytes), else kLaneKeepBytes.
+uint64_t lane_keep_bytes() {
+    const char* kb = std::getenv("DEOSS_LANE_KEEP_BYTES");
+    if (!kb || !*kb) return kLaneKeepBytes;
+    char* end = nullptr;
+    const unsigned long long v = std::strtoull(kb, &end, 10);
+    return (end != kb && *end == '\0' && kb[0] != '-') ? (uint64_t)v : kLaneKeepBytes;
+}
+
+// Lanes per GPU for a context over HIP devices devs[0 .. ndev) (devs NULL: device 0): the budget
+// of every one of its GPUs bounds it (each GPU gets the same count), in units of what each lane
+// will actually claim (lane_keep_bytes).
+int default_lanes(const int* devs, int ndev) {
     const char* v = std::getenv("DEOSS_LANES");
     if (v && *v) return std::min(std::max(std::atoi(v), 1), kMaxLanes);
-    size_t free_b = 0, total_b = 0;
-    if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
-        (void)hipGetLastError();
-        return 2;
+    const uint64_t keep = std::max<uint64_t>(lane_keep_bytes(), 1);
+    uint64_t lanes = 4;
+    const int n = (devs && ndev > 0) ? ndev : 1;
+    for (int i = 0; i < n; i++) {
+        const int dev = (devs && ndev > 0) ? devs[i] : 0;
+        size_t free_b = 0, total_b = 0;
+        if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();   // an unusable id: ctx_create rejects it
+            continue;
+        }
+        const uint64_t by_free = (uint64_t)free_b / (2 * keep);
+        const uint64_t half = (uint64_t)total_b / 2, claimed = keep_claimed(dev);
+        const uint64_t by_budget = claimed >= half ? 0 : (half - claimed) / keep;
+        lanes = std::min(lanes, std::max<uint64_t>(std::min(by_free, by_budget), 1));
     }
-    const uint64_t by_free = (uint64_t)free_b / (2 * kLaneKeepBytes);
-    const uint64_t half = (uint64_t)total_b / 2, claimed = keep_claimed(dev);
-    const uint64_t by_budget = claimed >= half ? 0 : (half - claimed) / kLaneKeepBytes;
-    return (int)std::min<uint64_t>(std::max<uint64_t>(std::min(by_free, by_budget), 1), 4);
+    return (int)lanes;
 }
 
 // An unforced multi-GPU context whose RCCL communicators could not be created keeps working with
@@ -1658,10 +1696,10 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
     c->lanes = lanes;
     c->devs.resize(ids.size() * (size_t)lanes);
     c->slots.reset(new DevSlot[c->devs.size()]);
-    const char* kb = std::getenv("DEOSS_LANE_KEEP_BYTES");
+    const uint64_t keep = lane_keep_bytes();
     for (size_t i = 0; i < c->devs.size(); i++) {   // lane-major: lane 0 of every GPU first
         c->devs[i].id = ids[i % ids.size()];
-        if (kb) c->devs[i].keep_bytes = std::strtoull(kb, nullptr, 10);
+        c->devs[i].keep_bytes = keep;
         int rc = init_device(c, c->devs[i]);
         if (rc != DM_OK) {
             dm_destroy(c);
@@ -1672,8 +1710,12 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
     c->keep_claimed = true;
     const char* fs = std::getenv("DEOSS_FORCE_SHARDED");
     c->force_sharded = fs != nullptr && fs[0] == '1';
+    c->route_k = dm_plan::route_constants_from_env();
     c->virtual_devs = nvirt > 1;
-    if ((ids.size() > 1 || c->force_sharded) && !c->virtual_devs) {   // every device's communicator up front: fail here, not mid-call
+    const char* tf = std::getenv("DEOSS_TEST_RCCL_INIT_FAIL");
+    c->fail_comm_init = tf && tf[0] == '1' && ids.size() > 1 && !c->force_sharded;
+    // every device's communicator up front: fail here, not mid-call
+    if ((ids.size() > 1 || c->force_sharded) && (!c->virtual_devs || c->fail_comm_init)) {
         std::vector<ncclComm_t>* cm = nullptr;
         const int rc = comms_for(c, (int)ids.size(), &cm);
         if (rc != DM_OK && c->force_sharded) {
@@ -1690,8 +1732,6 @@ int ctx_create(dm_ctx** out, const int* devs, int ndev, int lanes) {
             no_sharding(c, why.c_str());
         }
     }
-    const char* tf = std::getenv("DEOSS_TEST_RCCL_INIT_FAIL");   // test hook: the degraded path on one GPU
-    if (tf && tf[0] == '1' && ids.size() > 1 && !c->force_sharded) no_sharding(c, "DEOSS_TEST_RCCL_INIT_FAIL=1");
     *out = c;
     return DM_OK;
 }
@@ -1707,7 +1747,7 @@ int dm_create(dm_ctx** out, const int* devs, int ndev) {
     if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return set_err(DM_ERR_NODEV, "no usable GPU");
     if (first < 0 || first >= count) return bad_arg();
     std::lock_guard<std::mutex> lk(g_create_mu);
-    return ctx_create(out, devs, ndev, default_lanes(first));
+    return ctx_create(out, devs, ndev, default_lanes(devs, ndev));
 }
 
 int dm_create_lanes(dm_ctx** out, const int* devs, int ndev, int lanes) {
@@ -1835,7 +1875,15 @@ int dm_plan_route(uint64_t nleaves, uint64_t bytes, uint64_t leaf_max, int sourc
     if (ndev < 1 || cus < 1 || source < DM_SRC_DEVICE || source > DM_SRC_FILES || leaf_mode < DM_LEAF_AUTO ||
         leaf_mode > DM_LEAF_QUAD)
         return bad_arg();
-    return dm_plan::route(nleaves, bytes, leaf_max, source, ndev, cus, leaf_mode, busy, by_objects != 0, est_ms);
+    return dm_plan::route(nleaves, bytes, leaf_max, source, ndev, cus, leaf_mode, busy, by_objects != 0, est_ms,
+                          dm_plan::route_constants_from_env());
+}
+
+int dm_route_constants(dm_ctx* ctx, double* allgather_us, double* host_bytes_per_s) {
+    const dm_plan::RouteConstants k = ctx ? ctx->route_k : dm_plan::route_constants_from_env();
+    if (allgather_us) *allgather_us = k.allgather_ms * 1e3;
+    if (host_bytes_per_s) *host_bytes_per_s = k.host_bytes_per_s;
+    return DM_OK;
 }
 
 int dm_root_device_async(dm_ctx* ctx, const void* dev, uint64_t len, uint64_t chunk, void* dev_root,

@@ -19,7 +19,9 @@
 #pragma once
 
 #include <algorithm>
+#include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 namespace dm_plan {
@@ -116,7 +118,7 @@ inline double chip_bytes_per_s(int kind) {
 // Host-side feed per device (bytes/s): pinned memory crosses PCIe (zero-copy K1Q or H2D,
 // ~53-57 GB/s); pageable memory goes through a memcpy into the pinned ring first;
 // files are pread from the page cache by 4 threads per device.  Host memory is shared by all
-// devices: kHostBytesPerS caps the sum.
+// devices: RouteConstants::host_bytes_per_s caps the sum.
 inline double feed_bytes_per_s(int src) {
     switch (src) {
         case kSrcHostPinned: return 55e9;
@@ -125,16 +127,45 @@ inline double feed_bytes_per_s(int src) {
         default: return 0;
     }
 }
-constexpr double kHostBytesPerS = 500e9;   // 2-socket DDR5 host (~1.2 TB/s peak), PCIe reads + copies
+
+// The model's two terms no multi-GPU node has measured yet, as estimates: the all-gather of the
+// 32-byte subtree roots over RCCL (0.1 ms) and the host memory bandwidth all devices share (500
+// GB/s: a 2-socket DDR5 host, ~1.2 TB/s peak, serving PCIe reads and copies).  The N = 8 bench
+// line measures both and prints them as the environment variables that replace these at
+// dm_create (route_constants_from_env): DEOSS_ALLGATHER_US (exchange.avg_us) and
+// DEOSS_HOST_BYTES_PER_S (in_process.host_feed.all_GBps x 1e9), DESIGN.md §7.
+struct RouteConstants {
+    double allgather_ms = 0.10;
+    double host_bytes_per_s = 500e9;
+};
+
+// A positive finite number from environment variable `name`, else `fallback` (unset, empty,
+// malformed, negative or zero values are ignored).
+inline double env_positive(const char* name, double fallback) {
+    const char* v = std::getenv(name);
+    if (!v || !*v) return fallback;
+    char* end = nullptr;
+    const double x = std::strtod(v, &end);
+    return (end != v && *end == '\0' && std::isfinite(x) && x > 0) ? x : fallback;
+}
+
+inline RouteConstants route_constants_from_env() {
+    RouteConstants k;
+    k.allgather_ms = env_positive("DEOSS_ALLGATHER_US", k.allgather_ms * 1e3) * 1e-3;
+    k.host_bytes_per_s = env_positive("DEOSS_HOST_BYTES_PER_S", k.host_bytes_per_s);
+    return k;
+}
 // Fixed cost of a sharded call: a host thread per device, per-device setup, the gather of the
 // 32-byte nodes and the final levels on the first device.  Measured with G virtual devices on one
 // GPU (tools/shard_overhead.py, profiles/r03/LOGS.md#shard_overhead.log: +0.093 / 0.230 / 0.463 ms at
 // G = 2 / 4 / 8 over one device, i.e. ~0.06 ms per device), plus 0.1 ms for the all-gather of a
-// few KiB.  dm_exchange_timing measures that gather: 0.19 ms at G = 8 with virtual devices (the
+// few KiB (RouteConstants::allgather_ms).  dm_exchange_timing measures that gather: 0.19 ms at G = 8 with virtual devices (the
 // D2D stand-in, profiles/r04/LOGS.md#r04a_inproc.log); the RCCL gather over xGMI is recorded by the N = 8
 // bench line (other_configs.in_process.sharded_object.exchange).  Sharding needs a >= 5 % gain, so
 // an error in this sub-millisecond term can only change the choice for calls under ~10 ms.
-inline double shard_overhead_ms(int G) { return G > 1 ? 0.10 + 0.06 * G : 0.0; }
+inline double shard_overhead_ms(int G, double allgather_ms = RouteConstants().allgather_ms) {
+    return G > 1 ? allgather_ms + 0.06 * G : 0.0;
+}
 
 // Estimated time of one device hashing m leaves (longest leaf_max bytes, `bytes` in total) that
 // start at `src`; feed and hashing overlap (stripes / zero-copy), so the larger one bounds it.
@@ -153,16 +184,17 @@ inline double device_ms(uint64_t m, uint64_t bytes, uint64_t leaf_max, int src, 
 // one tree's aligned blocks (plan_shards, within 1/8 of even).  busy = calls already running or
 // queued on the context: a loaded context gains more from routing whole calls to idle devices than
 // from splitting one, so it never shards.  est_ms (nullable, G entries): the model's time for 1..G.
+// k: the all-gather and host-bandwidth terms (estimates, or measured values from the environment).
 inline int route(uint64_t n, uint64_t bytes, uint64_t leaf_max, int src, int G, int cus, int mode, int busy,
-                 bool by_objects = false, double* est_ms = nullptr) {
+                 bool by_objects = false, double* est_ms = nullptr, const RouteConstants& k = RouteConstants()) {
     int best = 1;
     double best_ms = 0;
     for (int g = 1; g <= std::max(1, G); g++) {
         const uint64_t m = by_objects ? ceil_div(n, (uint64_t)g) : plan_shards(n, g).max_leaves();
         const uint64_t b = n ? (uint64_t)((double)bytes * (double)m / (double)n) : 0;
         double t = device_ms(m, b, leaf_max, src, cus, mode);
-        if (src != kSrcDevice) t = std::max(t, (double)bytes / kHostBytesPerS * 1e3);
-        t += shard_overhead_ms(g);
+        if (src != kSrcDevice) t = std::max(t, (double)bytes / k.host_bytes_per_s * 1e3);
+        t += shard_overhead_ms(g, k.allgather_ms);
         if (est_ms) est_ms[g - 1] = t;
         if (g == 1) best_ms = t;
         else if (src != kSrcDevice && busy == 0 && n >= 2 && t < 0.95 * best_ms) {   // >= 5 % sooner

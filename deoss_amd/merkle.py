@@ -69,6 +69,14 @@ class MerkleContext:
         one GPU."""
         return bool(self._L.dm_can_shard(self._h))
 
+    def route_constants(self):
+        """(all-gather microseconds, host bytes/s) this context's routing model uses
+        (dm_route_constants): estimates, or DEOSS_ALLGATHER_US / DEOSS_HOST_BYTES_PER_S as set at
+        dm_create."""
+        ag, hb = ctypes.c_double(), ctypes.c_double()
+        self._check(self._L.dm_route_constants(self._h, ctypes.byref(ag), ctypes.byref(hb)), "dm_route_constants")
+        return ag.value, hb.value
+
     @staticmethod
     def keep_claimed(hip_device: int = 0) -> int:
         """Idle lane-buffer bytes every live context of this process may keep on that GPU

@@ -376,6 +376,13 @@ int dm_plan_shards(uint64_t nleaves, int ndev, uint32_t *levels, uint64_t *nbloc
  * model's time for 1 .. ndev devices. */
 int dm_plan_route(uint64_t nleaves, uint64_t bytes, uint64_t leaf_max, int source, int by_objects, int ndev, int cus,
                   int leaf_mode, int busy, double *est_ms);
+/* The cost model's two terms that only a multi-GPU node can measure: the all-gather of the
+ * 32-byte subtree roots (default 100 us) and the host memory bandwidth every device's feed shares
+ * (default 500e9 B/s).  Environment variables DEOSS_ALLGATHER_US and DEOSS_HOST_BYTES_PER_S
+ * (positive numbers; the N = 8 bench line prints the measured values as route_constants) replace
+ * them: read once by dm_create for its context, and per call by dm_plan_route.  The values a
+ * context uses (ctx NULL: what dm_plan_route would use now); either pointer nullable.  0. */
+int dm_route_constants(dm_ctx *ctx, double *allgather_us, double *host_bytes_per_s);
 
 /* ---- tuning ------------------------------------------------------------------------------ */
 

@@ -149,3 +149,89 @@ def test_strong_leg_error_and_missing_blocks():
     for k in REQUIRED:
         if k != "roofline":
             assert k in line, k
+
+
+def _n8_with_cpu_baseline(tmp_path):
+    """Round 4's N = 8 rehearsal line plus the cpu_baseline block an N > 1 run now carries (over
+    rank 0's shard: here the N = 1 line's block, the same 8 GiB object), written to a file."""
+    full = copy.deepcopy(_full_line("r04m_rehearse8.log"))
+    full["cpu_baseline"] = copy.deepcopy(_full_line("r04q_bench.log")["cpu_baseline"])
+    full["cpu_baseline"]["shard_root_bit_exact"] = True
+    path = tmp_path / "n8.json"
+    path.write_text(json.dumps(full))
+    return path
+
+
+def _fake(tmp_path, *extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "DEOSS_BENCH_T0")}
+    return [sys.executable, "bench.py", "--fake-legs", *extra, "--fake-line", str(_n8_with_cpu_baseline(tmp_path)),
+            "--detail-out", str(tmp_path / "d.json")], env
+
+
+def test_killed_mid_leg_leaves_a_parseable_line(tmp_path):
+    """the line is printed after the headline and after every leg, so a run the
+    driver kills in the middle of a leg (SIGKILL: no handler runs) still ends stdout with a whole
+    line that carries the headline, its roofline and its CPU baseline, and names the legs it did
+    not finish."""
+    import signal
+    import time
+    cmd, env = _fake(tmp_path, "3")
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                         start_new_session=True)
+    lines = []
+    try:
+        t0 = time.time()
+        while len(lines) < 2 and time.time() - t0 < 60:     # the headline, then the line after leg 1
+            ln = p.stdout.readline()
+            if not ln:
+                break
+            lines.append(ln)
+        assert len(lines) == 2, lines
+        time.sleep(0.5)                                     # now inside leg 2 (3 s)
+    finally:
+        os.killpg(p.pid, signal.SIGKILL)
+        rest = p.stdout.read()
+        p.wait(timeout=30)
+    assert p.returncode == -signal.SIGKILL
+    lines += [x for x in rest.splitlines(keepends=True) if x.strip()]
+    assert len(lines) == 2                                  # nothing was printed after the kill
+    for ln in lines:
+        assert len(ln.strip()) <= bench.LINE_MAX_BYTES
+    last = json.loads(lines[-1])
+    for k in REQUIRED + ("cpu_baseline", "legs", "complete"):
+        assert k in last, k
+    assert last["value"] > 0 and last["roofline"]["frac"] > 0 and last["cpu_baseline"]["cores"] == 1
+    assert last["cpu_baseline"]["shard_root_bit_exact"] is True
+    assert last["complete"] is False and last["legs"]["done"] == {"strong_scaling": last["legs"]["done"]["strong_scaling"]}
+    assert last["legs"]["pending"] == ["strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process"]
+    assert last["strong_scaling"]["bit_exact"] is True
+    first = json.loads(lines[0])
+    assert first["value"] == last["value"] and len(first["legs"]["pending"]) == 5
+
+
+def test_deadline_skips_legs_that_do_not_fit(tmp_path):
+    """--deadline-s: a leg starts only if its estimate fits in what is left; the skipped ones are
+    named in `problems` and `legs.skipped`, the run still ends with a complete line and status 0."""
+    cmd, env = _fake(tmp_path, "0.6")
+    r = subprocess.run(cmd + ["--deadline-s", "2.0"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = [json.loads(x) for x in r.stdout.splitlines() if x.strip()]
+    assert len(out) == 6                                     # the headline + one line per leg, run or skipped
+    last = out[-1]
+    assert last["complete"] is True and last["legs"]["pending"] == []
+    assert "strong_scaling" in last["legs"]["done"] and "in_process" in last["legs"]["skipped"]
+    assert set(last["legs"]["done"]) | set(last["legs"]["skipped"]) == {
+        "strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process"}
+    assert last["ok"] is False and "skipped:in_process" in last["problems"]
+    assert "deadline" in last["legs"]["skipped"]["in_process"]
+    with open(tmp_path / "d.json") as f:                   # the detail file is rewritten with every line
+        assert json.load(f)["legs"]["skipped"].keys() == last["legs"]["skipped"].keys()
+
+
+def test_leg_estimates_fit_the_default_deadline():
+    """The N = 8 legs' full-size estimates plus the headline fit the default
+    deadline, which leaves the driver's 600 s a margin; the in-process watchdog never outlives it."""
+    n8 = ("strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process")
+    headline_s = 90.0     # torch import + process group + 25 steps of 0.49 s + parity legs, with margin
+    assert headline_s + sum(bench.LEG_ESTIMATE_S[k] for k in n8) < bench.DEADLINE_DEFAULT_S < 600
+    assert bench.WATCHDOG_MARGIN_S > 0

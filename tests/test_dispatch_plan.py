@@ -118,6 +118,43 @@ def test_route_decision_table(lib, what, n, nbytes, leaf_max, src, want):
         assert min(est[1:]) >= 0.95 * est[0]   # no device count is >= 5 % sooner
 
 
+def route_constants(lib):
+    ag, hb = ctypes.c_double(), ctypes.c_double()
+    assert lib.dm_route_constants(None, ctypes.byref(ag), ctypes.byref(hb)) == 0
+    return ag.value, hb.value
+
+
+def test_route_constants_from_the_environment(lib, monkeypatch):
+    """the N = 8 bench line's measured all-gather and host-feed rates replace
+    the model's two estimates without a code change (DEOSS_ALLGATHER_US, DEOSS_HOST_BYTES_PER_S,
+    printed by that line as route_constants).  Each override flips the decision it governs."""
+    monkeypatch.delenv("DEOSS_ALLGATHER_US", raising=False)
+    monkeypatch.delenv("DEOSS_HOST_BYTES_PER_S", raising=False)
+    assert route_constants(lib) == (100.0, 500e9)
+    cfg3 = (32768, 1 << 40, 32 * MiB, "pinned")             # configs[3] from host: 8 GPUs by default
+    small = (2 * MiB, 8 * GiB, 4096, "pinned")             # 8 GiB @ 4 KiB: 8 GPUs by default
+    assert route(lib, *cfg3)[0] == 8 and route(lib, *small)[0] == 8
+    # a host that feeds all GPUs together no faster than one PCIe link: nothing gains from sharding
+    monkeypatch.setenv("DEOSS_HOST_BYTES_PER_S", "50e9")
+    assert route_constants(lib) == (100.0, 50e9)
+    assert route(lib, *cfg3)[0] == 1
+    monkeypatch.delenv("DEOSS_HOST_BYTES_PER_S")
+    # an all-gather of 1 s outweighs the 156 ms one GPU takes over PCIe
+    monkeypatch.setenv("DEOSS_ALLGATHER_US", "1000000")
+    assert route_constants(lib)[0] == 1e6
+    assert route(lib, *small)[0] == 1 and route(lib, *cfg3)[0] == 8   # 1 s is nothing against 20 s
+    # a measured all-gather of 41.5 us (what a real line would print) changes none of the table's decisions
+    monkeypatch.setenv("DEOSS_ALLGATHER_US", "41.5")
+    for what, n, nbytes, leaf_max, src, want in DECISIONS:
+        batch = src.endswith(" batch")
+        assert route(lib, n, nbytes, leaf_max, src.split()[0], by_objects=batch)[0] == want, what
+    # malformed, zero or negative values are ignored: the estimates stay
+    for bad in ("", "abc", "0", "-5", "1e400", "12us"):
+        monkeypatch.setenv("DEOSS_ALLGATHER_US", bad)
+        monkeypatch.setenv("DEOSS_HOST_BYTES_PER_S", bad)
+        assert route_constants(lib) == (100.0, 500e9), bad
+
+
 def test_route_never_shards_a_busy_context(lib):
     assert route(lib, 32768, 1 << 40, 32 * MiB, "pinned")[0] == 8
     assert route(lib, 32768, 1 << 40, 32 * MiB, "pinned", busy=1)[0] == 1
