@@ -93,7 +93,8 @@ inline int current_device() {
 // device's mutex, and every hipHostMalloc / hipHostFree under the host mutex.  Round 4 saw four
 // segfaults inside the HSA runtime (pthread_mutex_lock under hipMalloc) when a DevBuf growth ran
 // out of memory while a reaper's hipFree of a large block was still pending behind a running
-// chain.  tools/oom_free_race.hip separates the conditions; whatever its verdict,
+// chain.  A round-5 probe separated the conditions (profiles/r05/LOGS.md#oom_free_race.log);
+// whatever its verdict,
 // under these locks the library never has a hipMalloc in flight beside one of its own hipFrees on
 // that device, and dev_alloc never issues a hipMalloc that hipMemGetInfo says cannot succeed --
 // not on the first try and not on the retry after a reaper drain.  The cost: an allocation waits
@@ -216,7 +217,7 @@ struct PinnedBuf {
 };
 
 // Deferred release.  hipFree, hipFreeAsync and hipHostFree wait for ALL work queued on the device
-// (tools/free_sync_probe.hip, profiles/r03/LOGS.md#free_sync_probe.log: ~280 ms behind an unrelated 300 ms
+// (profiles/r03/LOGS.md#free_sync_probe.log: ~280 ms behind an unrelated 300 ms
 // kernel on another stream; hipMalloc and event calls do not wait).  So buffers a call no longer
 // needs go to the context's reaper thread, which frees them in order: the caller never waits for
 // other callers' kernels.  The same device-wide wait makes it safe: every use of a buffer was
@@ -998,11 +999,11 @@ bool pinned_view(const void* const* ptrs, const uint64_t* lens, uint64_t n, std:
 
 // Zero-copy: leaves in pinned host memory are read in place by K1Q over PCIe, without a copy
 // to HBM.  K1Q's producer lanes load 8 consecutive 64-byte blocks per leaf, so its reads cross
-// PCIe as whole lines.  Measured from torch-pinned memory (tools/zero_copy_diag.py,
-// profiles/r02/LOGS.md (r02s_zc_*.log)), zero-copy vs copy: 8 GiB as 256 x 32 MiB 15.81 vs 15.63 GiB/s (the
+// PCIe as whole lines.  Measured from torch-pinned memory (profiles/r02/LOGS.md, r02s_zc_*.log),
+// zero-copy vs copy: 8 GiB as 256 x 32 MiB 15.81 vs 15.63 GiB/s (the
 // chain rate either way, without the 8 GiB device copy), 8,192 x 1 MiB 53.2 vs 52.4 (PCIe),
 // batches of 1 MiB objects 51.5 vs 43.8 (4,096), 53.2 vs 46.9 (8,192), 49.4 vs 47.6 (12,500).
-// K1L, K1P and K1 reach only ~41 GB/s reading host memory (tools/zero_copy_probe.py), so the
+// K1L, K1P and K1 reach only ~41 GB/s reading host memory (profiles/r02/LOGS.md), so the
 // many-leaf (wide) regime still copies.  Auto mode only (a forced kernel keeps the copy
 // paths testable); DEOSS_ZERO_COPY=0 turns it off.
 bool zero_copy_regime(const dm_ctx* c, const Dev& d, uint64_t nleaves) {
@@ -1241,7 +1242,7 @@ int init_device(dm_ctx* c, Dev& d) {
     HIP_TRY(hipDeviceGetAttribute(&d.cus, hipDeviceAttributeMultiprocessorCount, d.id));
     // A process's ordinary HIP streams share GPU_MAX_HW_QUEUES (4) hardware queues per priority
     // level, assigned least-used at creation, and a kernel or copy waits behind anything queued
-    // before it on its queue (tools/hwq_probe.hip; tools/conc_probe.hip: 4 normal streams run side
+    // before it on its queue (profiles/r03/r03l_hwq.log; tools/conc_probe.hip: 4 normal streams run side
     // by side, a 5th waits).  Which queue a lane would get then depends on every stream the process
     // made before (torch's included): measured, two lanes' 0.5 s chains shared one queue after a
     // caller had created 4 streams (profiles/r03/LOGS.md#r03u_lanes.log).  A stream made with a CU mask gets
