@@ -439,7 +439,16 @@ def fake_legs(args) -> None:
         out = json.load(f)
     out.pop("other_configs", None)
     names = ["strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process"]
-    legs = Legs(out, args.detail_out, args.deadline_s, job_start_time(), lambda mine: mine,
+    world, rank = env_int("WORLD_SIZE", 1), env_int("RANK", 0)
+    decide, deadline = (lambda mine: mine), args.deadline_s
+    if world > 1:   # gloo ranks, no GPU: every rank must follow rank 0's decisions, whatever its own clock says
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        decide = lambda mine: _bcast_flag(torch, dist, mine, None)   # noqa: E731
+        if rank:
+            deadline = 0.0    # alone, a rank with no time left would skip every leg
+    legs = Legs(out, args.detail_out if rank == 0 else None, deadline, job_start_time(), decide,
                 estimates={n: args.fake_legs for n in names})
     legs.plan(names)
     legs.emit()
@@ -453,6 +462,12 @@ def fake_legs(args) -> None:
             out.setdefault("other_configs", {})[name] = {"bit_exact": True, "devices": 8} if name == "in_process" else r
     for name in names:
         legs.run(name, lambda name=name: leg(name))
+    if world > 1:
+        if rank and args.detail_out:
+            with open(f"{args.detail_out}.rank{rank}.json", "w") as f:
+                json.dump(out["legs"], f)
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def strong_scaling_leg(args, torch, dist, world, rank, device, dev_index, gloo, barrier, weak_per_gpu,

@@ -235,3 +235,20 @@ def test_leg_estimates_fit_the_default_deadline():
     headline_s = 90.0     # torch import + process group + 25 steps of 0.49 s + parity legs, with margin
     assert headline_s + sum(bench.LEG_ESTIMATE_S[k] for k in n8) < bench.DEADLINE_DEFAULT_S < 600
     assert bench.WATCHDOG_MARGIN_S > 0
+
+
+def test_ranks_follow_rank0_leg_decisions_gloo(tmp_path):
+    """N > 1 (2 gloo ranks, no GPU, started by bench.py's own self-launch): rank 0 decides whether
+    each leg fits and every rank follows -- here rank 1's own clock says no time is left, yet it
+    runs exactly the legs rank 0 runs, so the collectives inside a leg stay matched."""
+    cmd, env = _fake(tmp_path, "0.2")
+    env["MASTER_ADDR"] = "127.0.0.1"
+    r = subprocess.run(cmd[:2] + ["--gpus", "2"] + cmd[2:] + ["--deadline-s", "300"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    last = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert set(last["legs"]["done"]) == {"strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]",
+                                         "in_process"} and last["complete"] is True
+    with open(tmp_path / "d.json.rank1.json") as f:
+        r1 = json.load(f)
+    assert set(r1["done"]) == set(last["legs"]["done"]) and not r1["skipped"] and r1["deadline_s"] == 0.0
