@@ -54,7 +54,8 @@ def load_traffic(kind: str, n_leaves: int, alg_bytes: int = 0):
     key = f"{kind}:{grid}"
     e = d.get("by_kernel_grid", {}).get(key)
     if e:
-        return e["hbm_bytes_per_launch"], f"profiles/k1_traffic.json[{key}] <- " + d.get("source", "")
+        return e["hbm_bytes_per_launch"], f"profiles/k1_traffic.json[{key}] <- " + (e.get("round_files") or
+                                                                                  d.get("source", ""))
     same = [(abs(int(k.split(":")[1]) - grid), k, v) for k, v in d.get("by_kernel_grid", {}).items()
             if k.split(":")[0] == kind]
     if not same or not alg_bytes:
@@ -285,12 +286,17 @@ def main() -> None:
         dist.destroy_process_group()
 
 
-# Wall seconds each leg after the headline may take at full size (per-rank work, timed on one
-# MI355X: DESIGN.md §8, tools/n8_leg_times.sh), with a margin.  A leg starts only when its
-# estimate fits in what is left of --deadline-s; N = 1's extras and latency block total ~150 s.
+# Wall seconds each leg after the headline may take at full size.  The N = 8 legs' per-rank work
+# was timed on one MI355X as fresh processes (tools/n8_leg_times.sh, profiles/r06/n8_legs: the
+# 64 GiB single-GPU parity root 4.2 s, configs[1] at 4 KiB 2.3 s, configs[3]'s 128 GiB share
+# 4.2 s, configs[4]'s 12,500-object share 5.8 s, the in-process leg over 8 virtual devices and a
+# 64 GiB pinned object 27.8 s); each estimate is ~4x that, for a first RCCL init over 8 GPUs and
+# 8 ranks pinning host memory at once.  N = 1's extras were timed in the round-6
+# default run (profiles/r06/r06a_bench.log: 159 s in all).  A leg starts only when its estimate
+# fits in what is left of --deadline-s.
 LEG_ESTIMATE_S = {
-    "strong_scaling": 25.0, "strong_scaling_4KiB": 25.0, "configs[3]": 60.0, "configs[4]": 60.0,
-    "in_process": 150.0, "latency": 120.0, "FullProcessing_file": 45.0, "FullProcessing_while_receiving": 60.0,
+    "strong_scaling": 20.0, "strong_scaling_4KiB": 20.0, "configs[3]": 45.0, "configs[4]": 45.0,
+    "in_process": 120.0, "latency": 120.0, "FullProcessing_file": 45.0, "FullProcessing_while_receiving": 60.0,
 }
 LEG_ESTIMATE_DEFAULT_S = 20.0
 DEADLINE_DEFAULT_S = 540.0    # 90 % of the 600 s the driver gave the N = 1 bench (BENCH_r05.json)
@@ -911,6 +917,8 @@ def _extra_line(r):
         e.update({"bound": rf.get("bound"), "frac": _r(rf.get("frac"), 6)})
         if rf.get("traffic_over_algorithmic") is not None:
             e["traffic_x"] = rf["traffic_over_algorithmic"]
+        elif rf.get("traffic") and rf.get("algorithmic_bytes_per_launch"):
+            e["traffic_x"] = round(rf["traffic"] / rf["algorithmic_bytes_per_launch"], 5)
     cb = r.get("cpu_baseline")
     if isinstance(cb, dict) and cb.get("value") is not None:
         e["cpu"] = {"value": _r(cb["value"]), "cores": cb.get("cores")}

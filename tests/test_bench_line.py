@@ -229,12 +229,20 @@ def test_deadline_skips_legs_that_do_not_fit(tmp_path):
 
 
 def test_leg_estimates_fit_the_default_deadline():
-    """The N = 8 legs' full-size estimates plus the headline fit the default
-    deadline, which leaves the driver's 600 s a margin; the in-process watchdog never outlives it."""
+    """The N = 8 legs' estimates plus the headline fit the default deadline, which leaves the
+    driver's 600 s a margin; each estimate covers at least 3x the leg's per-rank work measured at
+    full size on one MI355X (profiles/r06/n8_legs/times.jsonl, tools/n8_leg_times.sh); the
+    in-process watchdog ends before the deadline."""
     n8 = ("strong_scaling", "strong_scaling_4KiB", "configs[3]", "configs[4]", "in_process")
-    headline_s = 90.0     # torch import + process group + 25 steps of 0.49 s + parity legs, with margin
+    headline_s = 120.0    # a fresh node's torch import + process group + 25 steps of 0.49 s + parity legs
     assert headline_s + sum(bench.LEG_ESTIMATE_S[k] for k in n8) < bench.DEADLINE_DEFAULT_S < 600
-    assert bench.WATCHDOG_MARGIN_S > 0
+    with open(os.path.join(ROOT, "profiles", "r06", "n8_legs", "times.jsonl")) as f:
+        measured = {d["leg"]: d["wall_s"] for d in map(json.loads, f) if d["rc"] == 0}
+    covers = {"strong_scaling_4KiB": "strong_4k_8g", "configs[3]": "cfg3_share_128g", "configs[4]": "cfg4_share_12500",
+              "in_process": "inprocess_8virt_64g"}
+    for leg, m in covers.items():
+        assert bench.LEG_ESTIMATE_S[leg] >= 3 * measured[m], (leg, measured[m])
+    assert 0 < bench.WATCHDOG_MARGIN_S < bench.LEG_ESTIMATE_S["in_process"]
 
 
 def test_ranks_follow_rank0_leg_decisions_gloo(tmp_path):
@@ -252,3 +260,48 @@ def test_ranks_follow_rank0_leg_decisions_gloo(tmp_path):
     with open(tmp_path / "d.json.rank1.json") as f:
         r1 = json.load(f)
     assert set(r1["done"]) == set(last["legs"]["done"]) and not r1["skipped"] and r1["deadline_s"] == 0.0
+
+
+def _r06(name):
+    with open(os.path.join(ROOT, "tests", "golden", "bench_lines_r06.json")) as f:
+        return json.load(f)[name]
+
+
+def test_n_gt_1_line_carries_cpu_baseline_and_traffic():
+    """VERDICT r5 item 2, on round 6's real N > 1 records (tests/golden/bench_lines_r06.json): the
+    rebuilt line of the 8-rank rehearsal and of the 2-rank full-size run carry `cpu_baseline` (the
+    1-thread restatement over rank 0's shard, the job-share rate, the host) and `roofline.traffic`
+    (PMC bytes of the same kernel and per-rank launch shape), within 6 KB."""
+    for name in ("n8", "n2"):
+        full = _r06(name)
+        line = bench.compact_line(full, f"gpurun_out/bench_detail_{name}.json")
+        assert _size(line) <= bench.LINE_MAX_BYTES, name
+        cb = line["cpu_baseline"]
+        assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 1.0, name
+        assert cb["parallel"]["cores"] >= 1 and cb["host"] and cb["shard_root_bit_exact"] is True, name
+        assert "rank 0's shard" in cb["sample"], name
+        rf = line["roofline"]
+        assert rf["traffic"] and 0.99 < rf["traffic_over_algorithmic"] < 1.01, name
+        assert line["legs"]["pending"] == [] and line["complete"] is True and line["ok"] is True, name
+        for k in REQUIRED + ("parity", "launch", "exchange", "strong_scaling", "strong_scaling_4KiB", "vs_cpu_share"):
+            assert k in line, (name, k)
+    n8 = bench.compact_line(_r06("n8"), None)
+    assert set(n8["extras"]) == {"configs[3]", "configs[4]", "in_process"}
+    assert n8["extras"]["configs[3]"]["fixture_bit_exact"] is True
+    n2 = bench.compact_line(_r06("n2"), None)
+    assert n2["parity"]["cpu_root"] == n2["parity"]["sharded_root"] and "weak_n2" in n2["parity"]["cpu_root_source"]
+    assert "route_constants" not in n2          # a one-GPU rehearsal's numbers are not a node's
+
+
+def test_route_constants_from_a_real_line():
+    """An N > 1 line over RCCL prints the two measured routing terms as the environment values
+    dm_create reads."""
+    full = copy.deepcopy(_r06("n8"))
+    full.pop("same_device", None)
+    full["exchange"]["backend"] = "nccl (RCCL)"
+    full["exchange"]["avg_us"] = 41.53
+    full["other_configs"]["in_process"]["host_feed"].update(all_GBps=401.7, consistent=True)
+    line = bench.compact_line(full, None)
+    assert line["route_constants"] == {"DEOSS_ALLGATHER_US": 41.5, "DEOSS_HOST_BYTES_PER_S": 401700000000}
+    full["other_configs"]["in_process"]["host_feed"]["consistent"] = False
+    assert bench.compact_line(full, None)["route_constants"] == {"DEOSS_ALLGATHER_US": 41.5}
