@@ -164,8 +164,7 @@ def main() -> None:
     progress(f"bench.py {' '.join(sys.argv[1:])}")
     import torch
     import torch.distributed as dist
-    from deoss_amd import MerkleContext, plan_shards
-    from deoss_amd.sharding import sharded_root
+    from deoss_amd import plan_shards
 
     world = env_int("WORLD_SIZE", 1)
     rank = env_int("RANK", 0)
@@ -208,6 +207,7 @@ def main() -> None:
         if world > 1 and dist.is_initialized():
             dist.destroy_process_group()
         return
+
     def barrier():
         if world > 1:
             if gloo:
