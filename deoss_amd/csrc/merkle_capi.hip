@@ -1402,7 +1402,11 @@ int multi_root(dm_ctx* c, int G, uint64_t n, const LeafProducer& produce, uint8_
         NCCL_TRY(ncclGroupStart());
         for (int g = 0; g < G; g++) {
             Dev& d = c->devs[g];
-            NCCL_TRY(ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream));
+            const ncclResult_t r = ncclAllGather(d.gather.u8(), d.gather.u8() + slot, slot, ncclUint8, (*comms)[g], d.stream);
+            if (r != ncclSuccess) {   // close the group first: an open one would swallow the next call's collectives
+                (void)ncclGroupEnd();
+                return fail(c, DM_ERR_RCCL, "ncclAllGather on device %d: %s", d.id, ncclGetErrorString(r));
+            }
         }
         NCCL_TRY(ncclGroupEnd());
     }
